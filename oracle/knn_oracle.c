@@ -1,0 +1,273 @@
+/*
+ * knn_oracle.c -- CPU restatement of the reference KNN hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker
+ * (or the labelled "port" CPU baseline).  The product path never links it.
+ *
+ * Pinned against the reference: tests/golden/ holds predictions, confusion
+ * matrices and top-k (distance bits, train index) lists captured from the
+ * reference compiled in this container (oracle/Makefile, target `golden`,
+ * harness oracle/ref_capture.cpp); tests/test_oracle.py checks this file
+ * against every one of them bit for bit.
+ *
+ * Compiled with -O2 -ffp-contract=off and no -ffast-math, so each
+ * `diff*diff` and `sum+=` rounds to fp32 exactly like the reference's
+ * x86 subss/mulss/addss sequence.
+ *
+ * Reference anchors (paths relative to srna99/KNN-using-p_threads-and-MPI):
+ *   distance()               main.cpp:14-23
+ *   KNN() insertion + vote   main.cpp:25-85
+ *   computeConfusionMatrix   main.cpp:87-100
+ *   computeAccuracy          main.cpp:102-112
+ *   pthreads partition       multi-thread.cpp:154-192
+ */
+#include <float.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <ctype.h>
+
+/* ------------------------------------------------------------------------ */
+/* distance: main.cpp:14-23.  Sequential i = 0..d-1, no sqrt, no FMA.         */
+/* ------------------------------------------------------------------------ */
+float oracle_distance(const float *a, const float *b, int d)
+{
+    float sum = 0.0f;
+    for (int i = 0; i < d; i++) {
+        float diff = a[i] - b[i];
+        sum += diff * diff;
+    }
+    return sum;
+}
+
+/* ------------------------------------------------------------------------ */
+/* One query, restated literally from main.cpp:40-82: a sorted interleaved   */
+/* candidates array initialised to FLT_MAX, first slot with dist < cand      */
+/* (strict) shifts the tail down; labels are stored as float and cast back   */
+/* to int for the bincount; argmax with strict '>' (ties -> smallest label). */
+/* The extra idx array records the train index of each slot (for top-k       */
+/* fixtures); it does not influence the result.                              */
+/* Returns the prediction, or -1 if fewer than k finite (< FLT_MAX)          */
+/* distances exist (the reference would index classCounts with INT_MIN).     */
+/* ------------------------------------------------------------------------ */
+static int oracle_query(const float *train, const float *train_label_f, int64_t nt,
+                        const float *q, int d, int64_t ld, int k, int C,
+                        float *cand, int32_t *cidx, int *counts,
+                        float *out_dist, int32_t *out_idx)
+{
+    for (int i = 0; i < 2 * k; i++) cand[i] = FLT_MAX;
+    for (int i = 0; i < k; i++) cidx[i] = -1;
+    for (int64_t t = 0; t < nt; t++) {
+        float dist = oracle_distance(q, train + t * ld, d);
+        for (int c = 0; c < k; c++) {
+            if (dist < cand[2 * c]) {
+                for (int x = k - 2; x >= c; x--) {
+                    cand[2 * x + 2] = cand[2 * x];
+                    cand[2 * x + 3] = cand[2 * x + 1];
+                    cidx[x + 1] = cidx[x];
+                }
+                cand[2 * c] = dist;
+                cand[2 * c + 1] = train_label_f[t];
+                cidx[c] = (int32_t)t;
+                break;
+            }
+        }
+    }
+    if (out_dist) for (int i = 0; i < k; i++) out_dist[i] = cand[2 * i];
+    if (out_idx) for (int i = 0; i < k; i++) out_idx[i] = cidx[i];
+    if (k > 0 && cidx[k - 1] < 0) return -1;
+    memset(counts, 0, sizeof(int) * (size_t)C);
+    for (int i = 0; i < k; i++) {
+        int lab = (int)cand[2 * i + 1];
+        if (lab < 0 || lab >= C) return -1;
+        counts[lab] += 1;
+    }
+    int max = -1, max_index = 0;
+    for (int i = 0; i < C; i++) {
+        if (counts[i] > max) { max = counts[i]; max_index = i; }
+    }
+    return max_index;
+}
+
+typedef struct {
+    const float *train; const float *lab_f; int64_t nt;
+    const float *test; int64_t q0, q1;
+    int d; int64_t ld; int k; int C;
+    int32_t *pred; float *topk_dist; int32_t *topk_idx;
+    int bad;
+} oracle_job;
+
+static void *oracle_worker(void *arg)
+{
+    oracle_job *j = (oracle_job *)arg;
+    int kk = j->k > 0 ? j->k : 1;
+    float *cand = (float *)malloc(sizeof(float) * 2 * (size_t)kk);
+    int32_t *cidx = (int32_t *)malloc(sizeof(int32_t) * (size_t)kk);
+    int *counts = (int *)malloc(sizeof(int) * (size_t)(j->C > 0 ? j->C : 1));
+    for (int64_t q = j->q0; q < j->q1; q++) {
+        int p;
+        if (j->k <= 0) {
+            p = 0; /* main.cpp:65-76 with an empty candidate set: argmax of zeros */
+        } else {
+            p = oracle_query(j->train, j->lab_f, j->nt, j->test + q * j->ld, j->d, j->ld,
+                             j->k, j->C, cand, cidx, counts,
+                             j->topk_dist ? j->topk_dist + q * j->k : NULL,
+                             j->topk_idx ? j->topk_idx + q * j->k : NULL);
+        }
+        if (p < 0) { j->bad = 1; p = 0; }
+        j->pred[q] = p;
+    }
+    free(cand); free(cidx); free(counts);
+    return NULL;
+}
+
+/*
+ * Predict queries [q0, q1) of `test` against all of `train`.
+ * Row-major features with leading dimension ld (>= d).  labels are int32
+ * (the reference's (int)(float)label, main.cpp:66).  Work is split over
+ * nthreads with the reference's pthreads rule (multi-thread.cpp:154-158:
+ * contiguous, remainder to the last worker).
+ * Returns 0, or 1 if some query had fewer than k finite neighbours or a
+ * label outside [0, C).
+ */
+int oracle_knn(const float *train, const int32_t *train_labels, int64_t nt,
+               const float *test, int64_t q0, int64_t q1, int d, int64_t ld,
+               int k, int C, int32_t *pred, float *topk_dist, int32_t *topk_idx,
+               int nthreads)
+{
+    if (nthreads < 1) nthreads = 1;
+    float *lab_f = (float *)malloc(sizeof(float) * (size_t)(nt > 0 ? nt : 1));
+    for (int64_t t = 0; t < nt; t++) lab_f[t] = (float)train_labels[t];
+    int64_t nq = q1 - q0;
+    int64_t per = nq / nthreads, left = nq % nthreads;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
+    oracle_job *jobs = (oracle_job *)calloc((size_t)nthreads, sizeof(oracle_job));
+    int64_t s = q0;
+    for (int w = 0; w < nthreads; w++) {
+        int64_t e = s + per + (w == nthreads - 1 ? left : 0);
+        oracle_job j = {train, lab_f, nt, test, s, e, d, ld, k, C, pred, topk_dist, topk_idx, 0};
+        jobs[w] = j;
+        s = e;
+    }
+    for (int w = 0; w < nthreads; w++) pthread_create(&th[w], NULL, oracle_worker, &jobs[w]);
+    int bad = 0;
+    for (int w = 0; w < nthreads; w++) { pthread_join(th[w], NULL); bad |= jobs[w].bad; }
+    free(th); free(jobs); free(lab_f);
+    return bad;
+}
+
+/* main.cpp:87-100: C x C row-major [true][pred]. */
+void oracle_confusion_matrix(const int32_t *pred, const int32_t *labels, int64_t n, int C,
+                             int32_t *cm)
+{
+    memset(cm, 0, sizeof(int32_t) * (size_t)C * (size_t)C);
+    for (int64_t i = 0; i < n; i++) cm[(int64_t)labels[i] * C + pred[i]]++;
+}
+
+/* main.cpp:102-112. */
+float oracle_accuracy(const int32_t *cm, int C, int64_t n)
+{
+    int ok = 0;
+    for (int i = 0; i < C; i++) ok += cm[i * C + i];
+    return ok / (float)n;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Synthetic generator: counter-based, keyed by               */
+/* (seed, stream, row, col) so CPU and GPU regenerate identical data.        */
+/* The product's HIP generator implements the same formula; the tests check  */
+/* them against each other bit for bit.                                      */
+/* ------------------------------------------------------------------------ */
+static inline uint64_t mix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+uint64_t oracle_hash(uint64_t seed, uint32_t stream, uint64_t row, uint32_t col)
+{
+    uint64_t x = (seed * 0x9E3779B97F4A7C15ULL) ^ ((uint64_t)stream * 0xD1B54A32D192ED03ULL);
+    x += row * 0xA0761D6478BD642FULL + (uint64_t)col * 0xE7037ED1A0B428DBULL;
+    return mix64(x);
+}
+
+/* kind 0: fp32 on the 2^-23 grid in [-1, 1); kind 1: bf16-exact k/128, k in [-128, 128). */
+float oracle_gen_value(uint64_t seed, uint32_t stream, uint64_t row, uint32_t col, int kind)
+{
+    uint32_t u = (uint32_t)(oracle_hash(seed, stream, row, col) >> 32);
+    if (kind == 1) return (float)((int32_t)(u >> 24) - 128) * (1.0f / 128.0f);
+    return (float)(int32_t)(u >> 8) * (1.0f / 8388608.0f) - 1.0f;
+}
+
+#define ORACLE_LABEL_COL 0xFFFFu
+int32_t oracle_gen_label(uint64_t seed, uint32_t stream, uint64_t row, int C)
+{
+    uint32_t u = (uint32_t)(oracle_hash(seed, stream, row, ORACLE_LABEL_COL) >> 32);
+    return (int32_t)(u % (uint32_t)C);
+}
+
+/* Fill rows [row0, row0+n) of a row-major [n][ld] block (pad columns = 0). */
+void oracle_gen_block(uint64_t seed, uint32_t stream, int64_t row0, int64_t n, int d, int64_t ld,
+                      int kind, float *out, int32_t *labels, int C)
+{
+    for (int64_t r = 0; r < n; r++) {
+        for (int c = 0; c < d; c++)
+            out[r * ld + c] = oracle_gen_value(seed, stream, (uint64_t)(row0 + r), (uint32_t)c, kind);
+        for (int64_t c = d; c < ld; c++) out[r * ld + c] = 0.0f;
+        if (labels) labels[r] = oracle_gen_label(seed, stream, (uint64_t)(row0 + r), C);
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Minimal ARFF reader for the NUMERIC-only datasets (tests only).           */
+/* Numeric fields use strtof, which the survey measured bit-identical to     */
+/* libarff's istringstream >> float for decimals (libarff/arff_utils.h:56).  */
+/* Layout: features row-major [n][ld], class = last attribute, (int)label.   */
+/* Returns 0 on success.  Call with feat == NULL to get n and nattr only.    */
+/* ------------------------------------------------------------------------ */
+int oracle_arff_read(const char *path, int64_t *n_out, int *nattr_out, int64_t ld,
+                     float *feat, int32_t *labels)
+{
+    FILE *f = fopen(path, "r");
+    if (!f) return 1;
+    char *line = NULL; size_t cap = 0; ssize_t len;
+    int nattr = 0, in_data = 0; int64_t n = 0;
+    float *row = NULL;
+    while ((len = getline(&line, &cap, f)) >= 0) {
+        char *p = line;
+        while (*p == ' ' || *p == '\t') p++;
+        if (*p == '%' || *p == '\n' || *p == '\0' || *p == '\r') continue;
+        if (!in_data) {
+            if (strncasecmp(p, "@attribute", 10) == 0) nattr++;
+            else if (strncasecmp(p, "@data", 5) == 0) {
+                in_data = 1;
+                row = (float *)malloc(sizeof(float) * (size_t)(nattr > 0 ? nattr : 1));
+            }
+            continue;
+        }
+        int c = 0;
+        while (*p && c < nattr) {
+            while (*p == ' ' || *p == '\t' || *p == ',') p++;
+            if (*p == '\n' || *p == '\0' || *p == '\r') break;
+            char *end;
+            row[c++] = strtof(p, &end);
+            if (end == p) { free(row); free(line); fclose(f); return 2; }
+            p = end;
+            while (*p && *p != ',' && *p != '\n') p++;
+        }
+        if (c != nattr) { free(row); free(line); fclose(f); return 3; }
+        if (feat) {
+            for (int i = 0; i < nattr - 1; i++) feat[n * ld + i] = row[i];
+            for (int64_t i = nattr - 1; i < ld; i++) feat[n * ld + i] = 0.0f;
+            labels[n] = (int32_t)row[nattr - 1];
+        }
+        n++;
+    }
+    free(row); free(line); fclose(f);
+    *n_out = n; *nattr_out = nattr;
+    return 0;
+}
