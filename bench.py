@@ -1,0 +1,174 @@
+"""Throughput bench of the KNN hot path (BASELINE.json metric: distance pairs/s).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config A|B] [--no-cpu-baseline]
+
+One process per GPU (torchrun for N > 1).  Workload A (default, BASELINE configs[2]):
+1,000,000 train x 100,000 query rows per GPU x 128-d fp32, k = 10, 10 classes, synthetic
+rows from the counter-based generator generated directly in HBM.  The test
+set is sharded (rank r owns query rows [r*nq, (r+1)*nq)), train is replicated: weak
+scaling with no data-path collective (the reference's MPI_Gatherv of predictions,
+mpi.cpp:186, is not part of the timed region).  A "step" is one KNN(train, test, k) pass
+over the resident inputs: norms -> MFMA filter -> exact rescore/vote -> fallback.
+
+Rank 0 prints one JSON line.  roofline: the dominant kernel (k_gemm_filter) timed with
+HIP events on its own stream; cpu_baseline: the reference's pthreads KNN (oracle/_ref,
+built -O0 as shipped) on a bounded sample, else the C restatement labelled "port".
+"""
+import argparse
+import glob
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+CONFIGS = {
+    # name: (n_train, n_query per GPU, d, k, classes, seed, scaling)
+    "A": (1_000_000, 100_000, 128, 10, 10, 1, "weak"),
+    "B": (4_000_000, 1_000_000, 64, 32, 10, 2, "strong"),
+}
+METRIC = "distance pairs/sec + queries/sec at 1/2/4/8 GPUs; accuracy bit-match"
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+
+
+def cpu_baseline(d, k, C, seed):
+    """Reference pthreads KNN (multi-thread.cpp:37) on a bounded sample of workload A."""
+    threads = int(os.environ.get("KNN_BENCH_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    nt_s, nq_s = 100_000, 64 * threads  # ~1e8 pairs: 10-30 s of CPU work at -O0
+    exe = os.path.join(REPO, "oracle", "_ref", "ref_bench")
+    sample = f"{nq_s} queries x {nt_s} train rows (d={d}, k={k}) of the same generator"
+    if os.path.exists(exe):
+        out = subprocess.run([exe, "0", str(seed), str(nt_s), str(nq_s), str(d), str(k), str(C),
+                              str(threads)], capture_output=True, text=True, check=True, timeout=600)
+        r = json.loads(out.stdout.strip().splitlines()[-1])
+        return {"value": r["pairs_per_s"], "unit": "pairs/s", "cores": threads, "kind": "reference",
+                "sample": sample + "; reference multi-thread.cpp KNN built -O0 as shipped",
+                "queries_per_s": r["queries_per_s"]}
+    # fallback: the C restatement (same algorithm, -O2), labelled as a port
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from conftest import Oracle
+    o = Oracle()
+    tr, tl = o.gen(seed, 0, 0, nt_s, d)
+    te, _ = o.gen(seed, 1, 0, nq_s, d)
+    t0 = time.perf_counter()
+    o.knn(tr, tl, te, k, C, threads=threads, topk=False)
+    dt = time.perf_counter() - t0
+    return {"value": nt_s * nq_s / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": sample + "; oracle/knn_oracle.c -O2", "queries_per_s": nq_s / dt}
+
+
+def pmc_traffic(round_tag=None):
+    """HBM bytes per k_gemm_filter launch from the committed rocprofv3 --pmc summary."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic*.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        return json.load(f).get("gemm_filter_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="A", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--algo", default="auto", choices=["auto", "gemm", "direct"])
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from importlib.util import module_from_spec, spec_from_file_location
+    spec = spec_from_file_location("knn_amd", os.path.join(REPO, "knn-using-p_threads-and-mpi_amd", "__init__.py"))
+    knn = module_from_spec(spec)
+    spec.loader.exec_module(knn)
+
+    nt, nq_cfg, d, k, C, seed, scaling = CONFIGS[args.config]
+    if scaling == "weak":
+        q0, nq = rank * nq_cfg, nq_cfg
+    else:
+        q0, q1 = knn.shard_range(nq_cfg, world, rank)
+        nq = q1 - q0
+    dev = torch.device("cuda", local)
+    ctx = knn.Context(local, algo=args.algo, profile=True)
+    train = torch.empty((nt, d), dtype=torch.float32, device=dev)
+    labels = torch.empty(nt, dtype=torch.int32, device=dev)
+    test = torch.empty((nq, d), dtype=torch.float32, device=dev)
+    ctx.generate(train, labels, 0, d, 0, seed, 0, C)   # train replicated on every rank
+    ctx.generate(test, None, q0, d, 0, seed, 1, C)     # this rank's query rows
+    pred = torch.empty(nq, dtype=torch.int32, device=dev)
+
+    def step():
+        ctx.predict_device(train, labels, test, k, C, pred)
+        return ctx.stage_times()
+
+    for _ in range(args.warmup):
+        step()
+    stage_sum = {}
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        for name, ms in step().items():
+            stage_sum[name] = stage_sum.get(name, 0.0) + ms
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    stats = ctx.stats()
+
+    if rank == 0:
+        total_q = nq_cfg * world if scaling == "weak" else nq_cfg
+        pairs = float(total_q) * nt * args.steps
+        stages = {n: v / args.steps for n, v in stage_sum.items()}
+        filt_ms = stages.get("gemm_filter")
+        roof = None
+        if filt_ms:
+            flops = 2.0 * d * nq * nt  # algorithmic: 2d FLOP per (query, train) pair, one launch
+            ach = flops / (filt_ms * 1e-3) / 1e12
+            roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                    "traffic": pmc_traffic(), "kernel": "k_gemm_filter",
+                    "algorithmic_flops_per_launch": flops, "avg_launch_ms": round(filt_ms, 3)}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(d, k, C, seed)
+        out = {
+            "metric": METRIC, "value": pairs / elapsed, "unit": "pairs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (counter-based generator, SURVEY.md 8d), generated in HBM",
+            "config": {"workload": f"{args.config}: synthetic {nt} train x {nq_cfg} query"
+                                   f"{'/GPU' if scaling == 'weak' else ''} x {d}-d fp32, k={k}",
+                       "n_train": nt, "n_query_total": total_q, "d": d, "k": k, "classes": C,
+                       "parallelism": f"test-sharded dp{world}, train replicated"},
+            "queries_per_s": total_q * args.steps / elapsed,
+            "stages_ms": {n: round(v, 3) for n, v in stages.items()},
+            "gemm_stats": stats,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,146 @@
+/*
+ * knn_amd.h -- C ABI of the MI355X-native KNN classifier (libknn_amd.so).
+ *
+ * Plain pointers and sizes only; no exceptions cross this boundary.  Every
+ * entry point below names the reference interface it replaces
+ * (srna99/KNN-using-p_threads-and-MPI, file:line).  The C++ surface that keeps
+ * the reference's own names (ArffParser / ArffData / KNN / computeConfusionMatrix
+ * / computeAccuracy) lives in knn_arff.hpp and is implemented on top of this ABI.
+ *
+ * Semantics (all paths, bit-exact with the reference serial KNN, main.cpp:25-85):
+ *   distance  = sum_{i<d} (q_i - t_i)^2, fp32, i ascending, no FMA (main.cpp:14-23)
+ *   neighbours= the k smallest (distance, train index) pairs -- the reference's
+ *               strict-'<' insertion queue keeps the lower index on ties
+ *               (main.cpp:45-61); distances >= FLT_MAX or NaN never qualify
+ *   vote      = bincount of the k labels, argmax with ties to the smallest label
+ *               (main.cpp:64-78)
+ * Data layout: row-major features [n][ld] (ld >= d elements, rows 16-B aligned
+ * for the device entry points), int32 labels in [0, num_classes).
+ */
+#ifndef KNN_AMD_H
+#define KNN_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KNN_AMD_ABI_VERSION 1
+
+typedef enum {
+    KNN_OK = 0,
+    KNN_EINVAL = 1,   /* bad argument: k > n_train, d mismatch, label outside [0,C), ... */
+    KNN_ENOMEM = 2,   /* host or device allocation failed */
+    KNN_EHIP = 3,     /* a HIP runtime call failed */
+    KNN_ERANGE = 4,   /* fewer than k neighbours with a finite distance (< FLT_MAX) */
+    KNN_ENODEV = 5,   /* no usable gfx950 device */
+    KNN_EIO = 6       /* file could not be opened / parsed (ARFF loader) */
+} knn_status;
+
+typedef enum { KNN_F32 = 0, KNN_BF16 = 1 } knn_dtype;
+
+typedef enum {
+    KNN_ALGO_AUTO = 0,    /* direct form for low d / small problems, MFMA GEMM form otherwise */
+    KNN_ALGO_DIRECT = 1,  /* fused direct-form distance + wave top-k + vote */
+    KNN_ALGO_GEMM = 2     /* ||q||^2+||t||^2-2q.t on FP32 MFMA + certified exact rescore */
+} knn_algo;
+
+/* Context options.  One context drives one device (one HIP stream). */
+typedef struct {
+    int32_t device;        /* HIP device ordinal */
+    int32_t algo;          /* knn_algo */
+    int32_t train_splits;  /* GEMM path: train segments per query tile (0 = auto) */
+    int32_t profile;       /* 1 = record per-stage HIP events (knn_stage_times) */
+} knn_opts;
+
+/* A dataset view.  feat: row-major [n][ld] of dtype; labels: int32 [n] (train only). */
+typedef struct {
+    const void* feat;
+    const int32_t* labels;
+    int64_t n;
+    int32_t d;
+    int32_t ld;
+    int32_t dtype;         /* knn_dtype */
+} knn_dataset;
+
+typedef struct knn_ctx knn_ctx;
+
+/* Library / ABI version (KNN_AMD_ABI_VERSION). */
+int32_t knn_version(void);
+
+/* Create / destroy a context (replaces the per-run setup in main.cpp:114-131,
+ * multi-thread.cpp:133-160 and mpi.cpp:119-149). */
+knn_status knn_create(knn_ctx** out, const knn_opts* opts);
+void knn_destroy(knn_ctx* ctx);
+
+/* Text of the last error on this context ("" if none). */
+const char* knn_last_error(const knn_ctx* ctx);
+
+/*
+ * Host-buffer entry point.  Replaces `int* KNN(ArffData* train, ArffData* test, int k)`
+ * (main.cpp:25) for queries [0, test->n) and the MPI variant
+ * `int* KNN(train, test, k, start, end)` (mpi.cpp:26) / pthreads thread body
+ * `void* KNN(void*)` (multi-thread.cpp:37) for a [q_begin, q_end) slice.
+ * out_pred: caller-allocated int32[q_end - q_begin].
+ * out_topk_dist / out_topk_idx: optional (NULL) [q_end-q_begin][k], ascending.
+ * k must satisfy 1 <= k <= train->n (the reference crashes for k > n_train and
+ * returns all-zero predictions for k <= 0; the C++ KNN() wrapper reproduces the
+ * latter, the ABI reports KNN_EINVAL).
+ */
+knn_status knn_predict(knn_ctx* ctx, const knn_dataset* train, const knn_dataset* test,
+                       int32_t k, int32_t num_classes, int64_t q_begin, int64_t q_end,
+                       int32_t* out_pred, float* out_topk_dist, int32_t* out_topk_idx);
+
+/*
+ * Device-buffer entry point (inputs already resident in HBM): all pointers in the
+ * datasets and outputs are device pointers on ctx's device; work is enqueued on
+ * `hip_stream` (a hipStream_t; NULL = the context's own stream).  Returns after
+ * the stream has drained and the device-side status word was checked.
+ */
+knn_status knn_predict_device(knn_ctx* ctx, const knn_dataset* train, const knn_dataset* test,
+                              int32_t k, int32_t num_classes, int32_t* d_pred,
+                              float* d_topk_dist, int32_t* d_topk_idx, void* hip_stream);
+
+/* Per-stage device times (ms) of the last predict call when opts.profile = 1.
+ * names: optional array of n const char* to receive stage names. Returns the
+ * number of stages recorded (<= n). */
+int32_t knn_stage_times(const knn_ctx* ctx, const char** names, float* ms, int32_t n);
+
+/* Counters of the last predict call: [0] GEMM candidates kept, [1] queries sent to
+ * the exact fallback, [2] train segments used.  Returns the number written. */
+int32_t knn_last_stats(const knn_ctx* ctx, int64_t* out, int32_t n);
+
+/*
+ * Synthetic generator, device side: fills rows [row0, row0+n) of a
+ * row-major [n][ld] device buffer (pad columns zeroed) and optional labels,
+ * from the counter-based hash keyed by (seed, stream, row, col).
+ * kind: 0 = fp32 on the 2^-23 grid in [-1,1), 1 = bf16-exact k/128.
+ * out dtype follows `dtype` (KNN_BF16 stores bf16 bits).
+ */
+knn_status knn_generate(knn_ctx* ctx, void* d_feat, int32_t* d_labels, int64_t row0, int64_t n,
+                        int32_t d, int32_t ld, int32_t dtype, int32_t kind, uint64_t seed,
+                        uint32_t stream, int32_t num_classes, void* hip_stream);
+
+/* Evaluation, host side.  computeConfusionMatrix (main.cpp:87-100): cm is
+ * caller-allocated int32[C*C], row = true class, col = predicted. */
+knn_status knn_confusion_matrix(const int32_t* pred, const int32_t* labels, int64_t n,
+                                int32_t num_classes, int32_t* cm);
+/* computeAccuracy (main.cpp:102-112): trace(cm) / n as float. */
+float knn_accuracy(const int32_t* cm, int32_t num_classes, int64_t n);
+
+/* ARFF loader (replaces ArffParser::parse, libarff/arff_parser.cpp:23, for the
+ * read path): NUMERIC attributes parsed with libarff's istringstream>>float rules.
+ * The class is the last attribute. */
+typedef struct knn_arff knn_arff;
+knn_status knn_arff_open(const char* path, knn_arff** out, char* err, int32_t err_len);
+void knn_arff_shape(const knn_arff* h, int64_t* n_instances, int32_t* n_attributes,
+                    int32_t* num_classes);
+/* Copies features [n][ld] (pad zeroed) and (int)(float) labels of the last attribute. */
+knn_status knn_arff_copy(const knn_arff* h, float* feat, int32_t ld, int32_t* labels);
+void knn_arff_close(knn_arff* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KNN_AMD_H */

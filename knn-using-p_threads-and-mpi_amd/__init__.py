@@ -1,0 +1,257 @@
+"""Python host mirror of the MI355X KNN path (ctypes over libknn_amd.so).
+
+The product is the C ABI in ``include/knn_amd.h`` (plus the reference-compatible C++
+API in ``include/knn_arff.hpp``); this module binds it for the tests and ``bench.py``.
+Names follow the reference (srna99/KNN-using-p_threads-and-MPI):
+
+* ``KNN(train, test, k)``                      main.cpp:25      -> int32 predictions
+* ``KNN_range(train, test, k, start, end)``    mpi.cpp:26 / multi-thread.cpp:37
+* ``computeConfusionMatrix(pred, labels, C)``  main.cpp:87
+* ``computeAccuracy(cm, n)``                   main.cpp:102
+* ``read_arff(path)``                          libarff ArffParser::parse (arff_parser.cpp:23)
+* ``shard_range(n, world, rank)``              multi-thread.cpp:154-158 / mpi.cpp:141-170
+
+There is no CPU fallback: if ``libknn_amd.so`` is missing or no gfx950 device is
+visible, calls raise ``KnnError``.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libknn_amd.so")
+
+KNN_OK, KNN_EINVAL, KNN_ENOMEM, KNN_EHIP, KNN_ERANGE, KNN_ENODEV, KNN_EIO = range(7)
+STATUS_NAMES = {0: "KNN_OK", 1: "KNN_EINVAL", 2: "KNN_ENOMEM", 3: "KNN_EHIP", 4: "KNN_ERANGE",
+                5: "KNN_ENODEV", 6: "KNN_EIO"}
+KNN_F32, KNN_BF16 = 0, 1
+ALGOS = {"auto": 0, "direct": 1, "gemm": 2}
+
+
+class KnnError(RuntimeError):
+    def __init__(self, status, msg=""):
+        self.status = status
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+
+
+class knn_opts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("algo", ctypes.c_int32),
+                ("train_splits", ctypes.c_int32), ("profile", ctypes.c_int32)]
+
+
+class knn_dataset(ctypes.Structure):
+    _fields_ = [("feat", ctypes.c_void_p), ("labels", ctypes.c_void_p), ("n", ctypes.c_int64),
+                ("d", ctypes.c_int32), ("ld", ctypes.c_int32), ("dtype", ctypes.c_int32)]
+
+
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Load libknn_amd.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise KnnError(KNN_ENODEV, f"{path} not built: run `make -C {_HERE}` "
+                                   "(or __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    P, I32, I64, F = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float
+    DS = ctypes.POINTER(knn_dataset)
+    sig = {
+        "knn_version": (I32, []),
+        "knn_create": (I32, [ctypes.POINTER(P), ctypes.POINTER(knn_opts)]),
+        "knn_destroy": (None, [P]),
+        "knn_last_error": (ctypes.c_char_p, [P]),
+        "knn_predict": (I32, [P, DS, DS, I32, I32, I64, I64, P, P, P]),
+        "knn_predict_device": (I32, [P, DS, DS, I32, I32, P, P, P, P]),
+        "knn_stage_times": (I32, [P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(F), I32]),
+        "knn_last_stats": (I32, [P, ctypes.POINTER(I64), I32]),
+        "knn_generate": (I32, [P, P, P, I64, I64, I32, I32, I32, I32, ctypes.c_uint64,
+                               ctypes.c_uint32, I32, P]),
+        "knn_confusion_matrix": (I32, [P, P, I64, I32, P]),
+        "knn_accuracy": (F, [P, I32, I64]),
+        "knn_arff_open": (I32, [ctypes.c_char_p, ctypes.POINTER(P), ctypes.c_char_p, I32]),
+        "knn_arff_shape": (None, [P, ctypes.POINTER(I64), ctypes.POINTER(I32), ctypes.POINTER(I32)]),
+        "knn_arff_copy": (I32, [P, P, I32, P]),
+        "knn_arff_close": (None, [P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _ptr(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def _dataset(feat, labels=None):
+    feat = np.ascontiguousarray(feat, dtype=np.float32)
+    if feat.ndim != 2:
+        raise KnnError(KNN_EINVAL, "features must be 2-D [n][d]")
+    lab = None if labels is None else np.ascontiguousarray(labels, dtype=np.int32)
+    ds = knn_dataset(feat.ctypes.data, None if lab is None else lab.ctypes.data, feat.shape[0],
+                     feat.shape[1], feat.shape[1], KNN_F32)
+    return ds, (feat, lab)  # keep the arrays alive
+
+
+def shard_range(n, world, rank):
+    """Contiguous split with the remainder on the last worker (multi-thread.cpp:154-158,
+    mpi.cpp:141-170): worker w < world-1 gets [w*(n//world), (w+1)*(n//world))."""
+    per, left = divmod(n, world)
+    start = rank * per
+    return start, start + per + (left if rank == world - 1 else 0)
+
+
+class Context:
+    """One device, one HIP stream (knn_create / knn_destroy)."""
+
+    def __init__(self, device=0, algo="auto", train_splits=0, profile=False):
+        self.lib = load_library()
+        opts = knn_opts(device, ALGOS[algo], train_splits, 1 if profile else 0)
+        h = ctypes.c_void_p()
+        st = self.lib.knn_create(ctypes.byref(h), ctypes.byref(opts))
+        if st != KNN_OK:
+            raise KnnError(st, f"knn_create(device={device}) failed")
+        self.h = h
+
+    def _check(self, st):
+        if st != KNN_OK:
+            raise KnnError(st, self.lib.knn_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.knn_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def predict(self, train_feat, train_labels, test_feat, k, num_classes=None, q_begin=0,
+                q_end=None, topk=False):
+        """Host arrays in, host arrays out (knn_predict)."""
+        tr, keep1 = _dataset(train_feat, train_labels)
+        te, keep2 = _dataset(test_feat)
+        if num_classes is None:
+            num_classes = int(keep1[1].max()) + 1 if keep1[1].size else 1
+        if q_end is None:
+            q_end = te.n
+        nq = q_end - q_begin
+        pred = np.zeros(max(nq, 0), np.int32)
+        dist = np.zeros((max(nq, 0), k), np.float32) if topk else None
+        idx = np.zeros((max(nq, 0), k), np.int32) if topk else None
+        self._check(self.lib.knn_predict(self.h, ctypes.byref(tr), ctypes.byref(te), k, num_classes,
+                                         q_begin, q_end, _ptr(pred), _ptr(dist), _ptr(idx)))
+        return (pred, dist, idx) if topk else pred
+
+    def predict_device(self, train, labels, test, k, num_classes, pred, dist=None, idx=None,
+                       stream=None, d=None):
+        """Device tensors (torch, on this context's device) in and out (knn_predict_device).
+        train/test: [n][ld] float32 contiguous; labels/pred/idx int32; dist float32."""
+        d = train.shape[1] if d is None else d
+        tr = knn_dataset(train.data_ptr(), labels.data_ptr(), train.shape[0], d, train.shape[1], KNN_F32)
+        te = knn_dataset(test.data_ptr(), None, test.shape[0], d, test.shape[1], KNN_F32)
+        self._check(self.lib.knn_predict_device(
+            self.h, ctypes.byref(tr), ctypes.byref(te), k, num_classes, pred.data_ptr(),
+            None if dist is None else dist.data_ptr(), None if idx is None else idx.data_ptr(),
+            None if stream is None else ctypes.c_void_p(stream)))
+
+    def generate(self, feat, labels, row0, d, kind, seed, stream_id, num_classes, dtype=KNN_F32,
+                 stream=None):
+        """Fill a device tensor [n][ld] (and labels) with the synthetic rows of SURVEY.md 8d."""
+        self._check(self.lib.knn_generate(
+            self.h, feat.data_ptr(), None if labels is None else labels.data_ptr(), row0,
+            feat.shape[0], d, feat.shape[1], dtype, kind, seed, stream_id, num_classes,
+            None if stream is None else ctypes.c_void_p(stream)))
+
+    def stage_times(self):
+        names = (ctypes.c_char_p * 16)()
+        ms = (ctypes.c_float * 16)()
+        n = self.lib.knn_stage_times(self.h, names, ms, 16)
+        out = {}
+        for i in range(n):
+            key = names[i].decode()
+            out[key] = out.get(key, 0.0) + ms[i]
+        return out
+
+    def stats(self):
+        v = (ctypes.c_int64 * 3)()
+        self.lib.knn_last_stats(self.h, v, 3)
+        return {"candidates": v[0], "fallback_queries": v[1], "train_segments": v[2]}
+
+
+_default_ctx = None
+
+
+def default_context():
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+def read_arff(path):
+    """Parse a NUMERIC ARFF file -> (features float32 [n][d], labels int32 [n], num_classes)."""
+    lib = load_library()
+    h = ctypes.c_void_p()
+    err = ctypes.create_string_buffer(512)
+    st = lib.knn_arff_open(os.fsencode(path), ctypes.byref(h), err, 512)
+    if st != KNN_OK:
+        raise KnnError(st, err.value.decode())
+    try:
+        n, na, C = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int32()
+        lib.knn_arff_shape(h, ctypes.byref(n), ctypes.byref(na), ctypes.byref(C))
+        d = na.value - 1
+        feat = np.zeros((n.value, max(d, 0)), np.float32)
+        labels = np.zeros(n.value, np.int32)
+        st = lib.knn_arff_copy(h, _ptr(feat), max(d, 0), _ptr(labels))
+        if st != KNN_OK:
+            raise KnnError(st, "non-numeric or missing value in " + str(path))
+        return feat, labels, C.value
+    finally:
+        lib.knn_arff_close(h)
+
+
+def KNN(train, test, k, ctx=None):
+    """main.cpp:25 -- train = (features, labels), test = features or (features, labels).
+    k <= 0 gives all-zero predictions like the reference."""
+    tf, tl = train
+    qf = test[0] if isinstance(test, tuple) else test
+    if k <= 0:
+        return np.zeros(len(qf), np.int32)
+    return (ctx or default_context()).predict(tf, tl, qf, k, int(np.max(tl)) + 1)
+
+
+def KNN_range(train, test, k, start, end, ctx=None):
+    """mpi.cpp:26 -- predictions for test rows [start, end)."""
+    tf, tl = train
+    qf = test[0] if isinstance(test, tuple) else test
+    if k <= 0:
+        return np.zeros(end - start, np.int32)
+    return (ctx or default_context()).predict(tf, tl, qf, k, int(np.max(tl)) + 1, start, end)
+
+
+def computeConfusionMatrix(predictions, labels, num_classes):
+    """main.cpp:87 -- [true][pred] counts, C x C int32."""
+    lib = load_library()
+    p = np.ascontiguousarray(predictions, np.int32)
+    lab = np.ascontiguousarray(labels, np.int32)
+    cm = np.zeros((num_classes, num_classes), np.int32)
+    st = lib.knn_confusion_matrix(_ptr(p), _ptr(lab), len(p), num_classes, _ptr(cm))
+    if st != KNN_OK:
+        raise KnnError(st, "label or prediction outside [0, num_classes)")
+    return cm
+
+
+def computeAccuracy(cm, n):
+    """main.cpp:102 -- trace / n as float32."""
+    lib = load_library()
+    cm = np.ascontiguousarray(cm, np.int32)
+    return float(np.float32(lib.knn_accuracy(_ptr(cm), cm.shape[0], n)))

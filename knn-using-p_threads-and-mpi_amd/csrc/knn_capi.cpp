@@ -1,0 +1,455 @@
+// knn_capi.cpp -- the C ABI (include/knn_amd.h): contexts, workspace, stage launches.
+//
+// Replaces the reference's drivers: the serial loop of main.cpp:25-85, the pthreads
+// fan-out of multi-thread.cpp:154-192 and the MPI scatter/gather of mpi.cpp:141-186
+// become one device pipeline per context:
+//   DIRECT:  k_exact_scan                                  (fused distance/top-k/vote)
+//   GEMM:    k_row_norms x2 -> k_gemm_filter -> k_rescore -> k_exact_scan(fallback list)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/knn_amd.h"
+#include "knn_kernels.h"
+
+namespace {
+
+struct DBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= bytes && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, n ? n : 16);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct Stage {
+    const char* name;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct knn_ctx {
+    int device = 0;
+    int algo = KNN_ALGO_AUTO;
+    int train_splits = 0;
+    int profile = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // device workspace
+    DBuf tnorm, qnorm, gthr, cnt, cand_idx, cand_L, cand_U, fb_list, ctrl;
+    // host-API staging (device copies of host inputs / outputs)
+    DBuf h_train, h_labels, h_test, h_pred, h_dist, h_idx;
+    int32_t* ctrl_host = nullptr;  // pinned: [0] status, [1] fallback count
+    // profiling
+    std::vector<hipEvent_t> events;
+    std::vector<Stage> stages;
+    std::vector<float> stage_ms;
+    std::vector<const char*> stage_names;
+    int64_t stats[3] = {0, 0, 0};
+    int num_cus = 256;
+};
+
+namespace {
+
+knn_status fail(knn_ctx* c, knn_status s, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
+knn_status fail(knn_ctx* c, knn_status s, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return s;
+}
+
+#define HIP_OR_FAIL(ctx, expr)                                                                  \
+    do {                                                                                        \
+        hipError_t e__ = (expr);                                                                \
+        if (e__ != hipSuccess)                                                                  \
+            return fail(ctx, e__ == hipErrorOutOfMemory ? KNN_ENOMEM : KNN_EHIP, "%s: %s (%s:%d)", \
+                        #expr, hipGetErrorString(e__), __FILE__, __LINE__);                    \
+    } while (0)
+
+// profiling helpers: events are created lazily and reused across calls
+void stage_begin(knn_ctx* c, hipStream_t st, const char* name) {
+    if (!c->profile) return;
+    size_t i = c->stages.size();
+    while (c->events.size() < 2 * (i + 1)) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        c->events.push_back(e);
+    }
+    Stage s{name, c->events[2 * i], c->events[2 * i + 1]};
+    c->stages.push_back(s);
+    (void)hipEventRecord(s.a, st);
+}
+void stage_end(knn_ctx* c, hipStream_t st) {
+    if (!c->profile || c->stages.empty()) return;
+    (void)hipEventRecord(c->stages.back().b, st);
+}
+
+knn_status check_dataset(knn_ctx* c, const knn_dataset* x, const char* what, bool need_labels) {
+    if (!x) return fail(c, KNN_EINVAL, "%s dataset is NULL", what);
+    if (x->n < 0) return fail(c, KNN_EINVAL, "%s: n < 0", what);
+    if (x->d <= 0) return fail(c, KNN_EINVAL, "%s: d must be > 0", what);
+    if (x->ld < x->d) return fail(c, KNN_EINVAL, "%s: ld < d", what);
+    if (x->dtype != KNN_F32) return fail(c, KNN_EINVAL, "%s: only KNN_F32 features are supported", what);
+    if (x->n > 0 && !x->feat) return fail(c, KNN_EINVAL, "%s: feat is NULL", what);
+    if (need_labels && x->n > 0 && !x->labels) return fail(c, KNN_EINVAL, "%s: labels are NULL", what);
+    return KNN_OK;
+}
+
+int choose_algo(const knn_ctx* c, int64_t nt, int64_t nq, int d, int k) {
+    if (c->algo == KNN_ALGO_DIRECT) return KNN_ALGO_DIRECT;
+    bool gemm_ok = d <= 128 && k <= 128 && knn_gemm_filter_lds(d <= 32 ? 32 : d <= 64 ? 64 : 128, k) <= 160 * 1024;
+    if (c->algo == KNN_ALGO_GEMM) return gemm_ok ? KNN_ALGO_GEMM : KNN_ALGO_DIRECT;
+    // AUTO: the direct form wins at low d (3 VALU ops per dim, no rescore) and on small jobs
+    if (gemm_ok && d >= 32 && nt >= 8192 && (double)nt * (double)nq >= 1e9) return KNN_ALGO_GEMM;
+    return KNN_ALGO_DIRECT;
+}
+
+knn_status finish_call(knn_ctx* c, hipStream_t st) {
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->ctrl_host, c->ctrl.p, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(c, hipStreamSynchronize(st));
+    if (c->profile) {
+        c->stage_ms.clear();
+        c->stage_names.clear();
+        for (auto& s : c->stages) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, s.a, s.b);
+            c->stage_ms.push_back(ms);
+            c->stage_names.push_back(s.name);
+        }
+    }
+    int32_t status = c->ctrl_host[0];
+    if (status & KNN_STATUS_BAD_LABEL) return fail(c, KNN_EINVAL, "a train label is outside [0, num_classes)");
+    if (status & KNN_STATUS_TOO_FEW) return fail(c, KNN_ERANGE, "fewer than k train rows have a finite distance (< FLT_MAX)");
+    return KNN_OK;
+}
+
+knn_status run_direct(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int k, int C,
+                      int32_t* pred, float* dist, int32_t* idx, hipStream_t st,
+                      const int32_t* qlist, const int32_t* qcount) {
+    ExactScanArgs a{};
+    a.train = (const float*)tr->feat; a.labels = tr->labels; a.nt = tr->n; a.ld_t = tr->ld;
+    a.test = (const float*)te->feat; a.ld_q = te->ld; a.nq = te->n;
+    a.d = tr->d; a.k = k; a.C = C;
+    a.qlist = qlist; a.qcount = qcount;
+    a.pred = pred; a.topk_dist = dist; a.topk_idx = idx; a.status = c->ctrl.as<int32_t>();
+    int grid = qlist ? std::max(1, 2 * c->num_cus) : (int)std::min<int64_t>(te->n, 16384);
+    if (grid <= 0) return KNN_OK;
+    HIP_OR_FAIL(c, knn_launch_exact_scan(a, grid, st));
+    return KNN_OK;
+}
+
+// GEMM-form certificate constants: Delta = coef*(qn+tn) + eta with
+// coef = (4d+32) u, eta = (6d+8) 2^-149, u = 2^-24.
+void certificate(int d, float* coef, float* eta) {
+    *coef = (float)(4 * d + 32) * 0x1p-24f;
+    *eta = (float)(6 * d + 8) * 0x1p-149f;
+}
+
+int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dk, int k) {
+    if (c->train_splits > 0) return c->train_splits;
+    int occ = 1;
+    if (knn_gemm_filter_occupancy(dk, k, &occ) != hipSuccess || occ < 1) occ = 1;
+    int64_t slots = (int64_t)occ * c->num_cus;
+    int best = 1;
+    double best_eff = 0.0;
+    for (int s = 1; s <= 8; s++) {
+        if (nt / s < 64 * 64) break;  // keep segments long enough to amortise the warm-up
+        int64_t w = n_qtiles * s;
+        double eff = (double)w / (double)(((w + slots - 1) / slots) * slots);
+        if (eff > best_eff + 0.02) { best = s; best_eff = eff; }
+        if (eff >= 0.9) break;
+    }
+    return best;
+}
+
+knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int k, int C,
+                    int32_t* pred, float* dist, int32_t* idx, hipStream_t st, bool* fell_back) {
+    *fell_back = false;
+    const int64_t nt = tr->n, nq = te->n;
+    const int d = tr->d;
+    const int dk = d <= 32 ? 32 : d <= 64 ? 64 : 128;
+    const int cap = 64 * KNN_RESCORE_CAPW;
+    HIP_OR_FAIL(c, c->tnorm.ensure(sizeof(float) * nt));
+    HIP_OR_FAIL(c, c->qnorm.ensure(sizeof(float) * nq));
+    HIP_OR_FAIL(c, c->gthr.ensure(sizeof(uint32_t) * nq));
+    HIP_OR_FAIL(c, c->cnt.ensure(sizeof(int32_t) * nq));
+    HIP_OR_FAIL(c, c->cand_idx.ensure(sizeof(int32_t) * nq * cap));
+    HIP_OR_FAIL(c, c->cand_L.ensure(sizeof(float) * nq * cap));
+    HIP_OR_FAIL(c, c->cand_U.ensure(sizeof(float) * nq * cap));
+    HIP_OR_FAIL(c, c->fb_list.ensure(sizeof(int32_t) * nq));
+
+    stage_begin(c, st, "norms");
+    HIP_OR_FAIL(c, knn_launch_row_norms((const float*)tr->feat, nt, tr->ld, d, c->tnorm.as<float>(), c->ctrl.as<int32_t>(), st));
+    HIP_OR_FAIL(c, knn_launch_row_norms((const float*)te->feat, nq, te->ld, d, c->qnorm.as<float>(), c->ctrl.as<int32_t>(), st));
+    stage_end(c, st);
+    // the certificate needs every norm < 2^125; otherwise take the exact path
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->ctrl_host, c->ctrl.p, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(c, hipStreamSynchronize(st));
+    if (c->ctrl_host[0] & KNN_STATUS_GEMM_UNSAFE) {
+        HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st));
+        *fell_back = true;
+        stage_begin(c, st, "exact_scan");
+        knn_status s = run_direct(c, tr, te, k, C, pred, dist, idx, st, nullptr, nullptr);
+        stage_end(c, st);
+        return s;
+    }
+
+    stage_begin(c, st, "filter_init");
+    HIP_OR_FAIL(c, hipMemsetAsync(c->cnt.p, 0, sizeof(int32_t) * nq, st));
+    HIP_OR_FAIL(c, hipMemsetD32Async((hipDeviceptr_t)c->gthr.p, 0xFF800000u, nq, st));  // ordered(+inf)
+    stage_end(c, st);
+
+    const int64_t n_qtiles = (nq + 127) / 128;
+    const int nseg = choose_splits(c, n_qtiles, nt, dk, k);
+    int64_t seg_len = (nt + nseg - 1) / nseg;
+    seg_len = (seg_len + 63) / 64 * 64;
+    GemmFilterArgs g{};
+    g.train = (const float*)tr->feat; g.nt = nt; g.ld_t = tr->ld;
+    g.test = (const float*)te->feat; g.nq = nq; g.ld_q = te->ld; g.d = d;
+    g.tnorm = c->tnorm.as<float>(); g.qnorm = c->qnorm.as<float>();
+    g.k = k; g.seg_len = seg_len; g.nseg = nseg; g.n_qtiles = (int)n_qtiles;
+    certificate(d, &g.coef, &g.eta);
+    g.gthr = c->gthr.as<uint32_t>();
+    g.cnt = c->cnt.as<int32_t>(); g.cand_idx = c->cand_idx.as<int32_t>();
+    g.cand_L = c->cand_L.as<float>(); g.cand_U = c->cand_U.as<float>(); g.cap = cap;
+    stage_begin(c, st, "gemm_filter");
+    HIP_OR_FAIL(c, knn_launch_gemm_filter(g, dk, st));
+    stage_end(c, st);
+
+    RescoreArgs r{};
+    r.train = (const float*)tr->feat; r.labels = tr->labels; r.ld_t = tr->ld;
+    r.test = (const float*)te->feat; r.ld_q = te->ld; r.nq = nq; r.d = d; r.k = k; r.C = C;
+    r.cnt = g.cnt; r.cand_idx = g.cand_idx; r.cand_L = g.cand_L; r.cand_U = g.cand_U; r.cap = cap;
+    r.pred = pred; r.topk_dist = dist; r.topk_idx = idx; r.status = c->ctrl.as<int32_t>();
+    r.fb_list = c->fb_list.as<int32_t>(); r.fb_count = c->ctrl.as<int32_t>() + 1;
+    stage_begin(c, st, "rescore");
+    HIP_OR_FAIL(c, knn_launch_rescore(r, st));
+    stage_end(c, st);
+
+    stage_begin(c, st, "fallback_scan");
+    knn_status s = run_direct(c, tr, te, k, C, pred, dist, idx, st, r.fb_list, r.fb_count);
+    stage_end(c, st);
+    c->stats[2] = nseg;
+    return s;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t knn_version(void) { return KNN_AMD_ABI_VERSION; }
+
+knn_status knn_create(knn_ctx** out, const knn_opts* opts) {
+    if (!out) return KNN_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return KNN_ENODEV;
+    knn_ctx* c = new (std::nothrow) knn_ctx();
+    if (!c) return KNN_ENOMEM;
+    if (opts) {
+        c->device = opts->device;
+        c->algo = opts->algo;
+        c->train_splits = opts->train_splits;
+        c->profile = opts->profile;
+    }
+    if (c->device < 0 || c->device >= ndev) { delete c; return KNN_ENODEV; }
+    hipDeviceProp_t prop;
+    if (hipSetDevice(c->device) != hipSuccess || hipGetDeviceProperties(&prop, c->device) != hipSuccess) {
+        delete c;
+        return KNN_ENODEV;
+    }
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        // kernels are built for gfx950 only
+        delete c;
+        return KNN_ENODEV;
+    }
+    c->num_cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void**)&c->ctrl_host, 4 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess ||
+        c->ctrl.ensure(4 * sizeof(int32_t)) != hipSuccess) {
+        knn_destroy(c);
+        return KNN_EHIP;
+    }
+    *out = c;
+    return KNN_OK;
+}
+
+void knn_destroy(knn_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    for (DBuf* b : {&c->tnorm, &c->qnorm, &c->gthr, &c->cnt, &c->cand_idx, &c->cand_L, &c->cand_U,
+                    &c->fb_list, &c->ctrl, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
+                    &c->h_dist, &c->h_idx})
+        b->release();
+    for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
+    if (c->ctrl_host) (void)hipHostFree(c->ctrl_host);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* knn_last_error(const knn_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+knn_status knn_predict_device(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int32_t k,
+                              int32_t C, int32_t* pred, float* dist, int32_t* idx, void* hip_stream) {
+    if (!c) return KNN_EINVAL;
+    c->err.clear();
+    knn_status s;
+    if ((s = check_dataset(c, tr, "train", true)) != KNN_OK) return s;
+    if ((s = check_dataset(c, te, "test", false)) != KNN_OK) return s;
+    if (tr->d != te->d) return fail(c, KNN_EINVAL, "feature count mismatch: train d=%d test d=%d", tr->d, te->d);
+    if (k < 1 || k > tr->n) return fail(c, KNN_EINVAL, "k=%d outside [1, n_train=%lld]", k, (long long)tr->n);
+    if (k > 1024) return fail(c, KNN_EINVAL, "k=%d exceeds the supported maximum 1024", k);
+    if (C < 1 || C > 16384) return fail(c, KNN_EINVAL, "num_classes=%d outside [1, 16384]", C);
+    if (tr->n > 0x7fffffffLL) return fail(c, KNN_EINVAL, "n_train exceeds 2^31-1");
+    if ((tr->ld & 3) || (te->ld & 3) || (((uintptr_t)tr->feat) & 15) || (((uintptr_t)te->feat) & 15))
+        return fail(c, KNN_EINVAL, "device rows must be 16-byte aligned (ld %% 4 == 0)");
+    if (te->n > 0 && !pred) return fail(c, KNN_EINVAL, "pred is NULL");
+    HIP_OR_FAIL(c, hipSetDevice(c->device));
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    c->stages.clear();
+    c->stats[0] = c->stats[1] = c->stats[2] = 0;
+    if (te->n == 0) return KNN_OK;
+    HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st));
+    int algo = choose_algo(c, tr->n, te->n, tr->d, k);
+    if (algo == KNN_ALGO_GEMM) {
+        bool fb = false;
+        if ((s = run_gemm(c, tr, te, k, C, pred, dist, idx, st, &fb)) != KNN_OK) return s;
+    } else {
+        stage_begin(c, st, "exact_scan");
+        if ((s = run_direct(c, tr, te, k, C, pred, dist, idx, st, nullptr, nullptr)) != KNN_OK) return s;
+        stage_end(c, st);
+    }
+    s = finish_call(c, st);
+    c->stats[1] = c->ctrl_host[1];
+    if (c->profile >= 2 && algo == KNN_ALGO_GEMM) {
+        // diagnostic only: total candidates kept by the filter
+        std::vector<int32_t> h(te->n);
+        if (hipMemcpy(h.data(), c->cnt.p, sizeof(int32_t) * te->n, hipMemcpyDeviceToHost) == hipSuccess) {
+            int64_t tot = 0;
+            for (int32_t v : h) tot += v;
+            c->stats[0] = tot;
+        }
+    }
+    return s;
+}
+
+knn_status knn_predict(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int32_t k, int32_t C,
+                       int64_t q_begin, int64_t q_end, int32_t* out_pred, float* out_dist,
+                       int32_t* out_idx) {
+    if (!c) return KNN_EINVAL;
+    c->err.clear();
+    knn_status s;
+    if ((s = check_dataset(c, tr, "train", true)) != KNN_OK) return s;
+    if ((s = check_dataset(c, te, "test", false)) != KNN_OK) return s;
+    if (q_begin < 0 || q_end < q_begin || q_end > te->n)
+        return fail(c, KNN_EINVAL, "query range [%lld, %lld) outside [0, %lld)", (long long)q_begin,
+                    (long long)q_end, (long long)te->n);
+    if (tr->d != te->d) return fail(c, KNN_EINVAL, "feature count mismatch: train d=%d test d=%d", tr->d, te->d);
+    if (k < 1 || k > tr->n) return fail(c, KNN_EINVAL, "k=%d outside [1, n_train=%lld]", k, (long long)tr->n);
+    const int64_t nq = q_end - q_begin;
+    if (nq == 0) return KNN_OK;
+    if (!out_pred) return fail(c, KNN_EINVAL, "out_pred is NULL");
+    HIP_OR_FAIL(c, hipSetDevice(c->device));
+    const int d = tr->d;
+    const int ldd = (d + 3) & ~3;  // device rows padded to 16 B
+    hipStream_t st = c->stream;
+    HIP_OR_FAIL(c, c->h_train.ensure(sizeof(float) * (size_t)ldd * tr->n));
+    HIP_OR_FAIL(c, c->h_labels.ensure(sizeof(int32_t) * tr->n));
+    HIP_OR_FAIL(c, c->h_test.ensure(sizeof(float) * (size_t)ldd * nq));
+    HIP_OR_FAIL(c, c->h_pred.ensure(sizeof(int32_t) * nq));
+    if (out_dist) HIP_OR_FAIL(c, c->h_dist.ensure(sizeof(float) * nq * k));
+    if (out_idx) HIP_OR_FAIL(c, c->h_idx.ensure(sizeof(int32_t) * nq * k));
+    HIP_OR_FAIL(c, hipMemcpy2DAsync(c->h_train.p, sizeof(float) * ldd, tr->feat, sizeof(float) * tr->ld,
+                                    sizeof(float) * d, tr->n, hipMemcpyHostToDevice, st));
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->h_labels.p, tr->labels, sizeof(int32_t) * tr->n, hipMemcpyHostToDevice, st));
+    HIP_OR_FAIL(c, hipMemcpy2DAsync(c->h_test.p, sizeof(float) * ldd,
+                                    (const float*)te->feat + q_begin * te->ld, sizeof(float) * te->ld,
+                                    sizeof(float) * d, nq, hipMemcpyHostToDevice, st));
+    knn_dataset dtr{c->h_train.p, c->h_labels.as<int32_t>(), tr->n, d, ldd, KNN_F32};
+    knn_dataset dte{c->h_test.p, nullptr, nq, d, ldd, KNN_F32};
+    s = knn_predict_device(c, &dtr, &dte, k, C, c->h_pred.as<int32_t>(),
+                           out_dist ? c->h_dist.as<float>() : nullptr,
+                           out_idx ? c->h_idx.as<int32_t>() : nullptr, st);
+    if (s != KNN_OK) return s;
+    HIP_OR_FAIL(c, hipMemcpyAsync(out_pred, c->h_pred.p, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, st));
+    if (out_dist) HIP_OR_FAIL(c, hipMemcpyAsync(out_dist, c->h_dist.p, sizeof(float) * nq * k, hipMemcpyDeviceToHost, st));
+    if (out_idx) HIP_OR_FAIL(c, hipMemcpyAsync(out_idx, c->h_idx.p, sizeof(int32_t) * nq * k, hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(c, hipStreamSynchronize(st));
+    return KNN_OK;
+}
+
+int32_t knn_stage_times(const knn_ctx* c, const char** names, float* ms, int32_t n) {
+    if (!c) return 0;
+    int32_t m = (int32_t)std::min<size_t>((size_t)std::max(n, 0), c->stage_ms.size());
+    for (int32_t i = 0; i < m; i++) {
+        if (names) names[i] = c->stage_names[i];
+        if (ms) ms[i] = c->stage_ms[i];
+    }
+    return m;
+}
+
+int32_t knn_last_stats(const knn_ctx* c, int64_t* out, int32_t n) {
+    if (!c || !out) return 0;
+    int32_t m = std::min(n, 3);
+    for (int32_t i = 0; i < m; i++) out[i] = c->stats[i];
+    return m;
+}
+
+knn_status knn_generate(knn_ctx* c, void* d_feat, int32_t* d_labels, int64_t row0, int64_t n, int32_t d,
+                        int32_t ld, int32_t dtype, int32_t kind, uint64_t seed, uint32_t stream,
+                        int32_t C, void* hip_stream) {
+    if (!c) return KNN_EINVAL;
+    if (n < 0 || d <= 0 || ld < d || (d_labels && C < 1) || (n > 0 && !d_feat) || (kind != 0 && kind != 1) ||
+        (dtype != KNN_F32 && dtype != KNN_BF16))
+        return fail(c, KNN_EINVAL, "knn_generate: bad arguments");
+    if (dtype == KNN_BF16 && kind != 1) return fail(c, KNN_EINVAL, "bf16 output needs kind=1 (bf16-exact values)");
+    HIP_OR_FAIL(c, hipSetDevice(c->device));
+    GenerateArgs a{d_feat, d_labels, row0, n, d, ld, dtype == KNN_BF16, kind, seed, stream, C};
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    HIP_OR_FAIL(c, knn_launch_generate(a, st));
+    HIP_OR_FAIL(c, hipStreamSynchronize(st));
+    return KNN_OK;
+}
+
+knn_status knn_confusion_matrix(const int32_t* pred, const int32_t* labels, int64_t n, int32_t C, int32_t* cm) {
+    if (!cm || C < 1 || n < 0 || (n > 0 && (!pred || !labels))) return KNN_EINVAL;
+    std::memset(cm, 0, sizeof(int32_t) * (size_t)C * (size_t)C);
+    for (int64_t i = 0; i < n; i++) {
+        int32_t t = labels[i], p = pred[i];
+        if (t < 0 || t >= C || p < 0 || p >= C) return KNN_EINVAL;  // the reference writes out of bounds here
+        cm[(int64_t)t * C + p]++;
+    }
+    return KNN_OK;
+}
+
+float knn_accuracy(const int32_t* cm, int32_t C, int64_t n) {
+    int ok = 0;
+    for (int32_t i = 0; i < C; i++) ok += cm[(int64_t)i * C + i];
+    return ok / (float)n;
+}
+
+}  // extern "C"

@@ -1,0 +1,55 @@
+// knn_kernels.h -- kernel argument blocks and host launchers (internal to libknn_amd).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// device status word bits (one int32 per predict call)
+#define KNN_STATUS_TOO_FEW 1       // a query has fewer than k finite distances
+#define KNN_STATUS_BAD_LABEL 2     // a neighbour's label is outside [0, C)
+#define KNN_STATUS_GEMM_UNSAFE 4   // a row norm is too large for the GEMM certificate
+
+// candidate-list capacity per query on the GEMM path (entries = 64 * CAPW)
+#define KNN_RESCORE_CAPW 16
+
+struct ExactScanArgs {
+    const float* train; const int32_t* labels; int64_t nt; int ld_t;
+    const float* test; int ld_q; int64_t nq;
+    int d; int k; int C;
+    const int32_t* qlist; const int32_t* qcount;  // optional query list (device count)
+    int32_t* pred; float* topk_dist; int32_t* topk_idx; int32_t* status;
+    int q_lds_bytes;                              // set by the launcher
+};
+
+struct GemmFilterArgs {
+    const float* train; int64_t nt; int ld_t;
+    const float* test; int64_t nq; int ld_q; int d;
+    const float* tnorm; const float* qnorm;
+    int k; int64_t seg_len; int nseg; int n_qtiles;
+    float coef; float eta;
+    uint32_t* gthr;
+    int32_t* cnt; int32_t* cand_idx; float* cand_L; float* cand_U; int cap;
+};
+
+struct RescoreArgs {
+    const float* train; const int32_t* labels; int ld_t;
+    const float* test; int ld_q; int64_t nq; int d; int k; int C;
+    const int32_t* cnt; const int32_t* cand_idx; const float* cand_L; const float* cand_U; int cap;
+    int32_t* pred; float* topk_dist; int32_t* topk_idx; int32_t* status;
+    int32_t* fb_list; int32_t* fb_count;
+    int q_lds_bytes; int c_lds_bytes; int wave_lds_bytes;  // set by the launcher
+};
+
+struct GenerateArgs {
+    void* out; int32_t* labels; int64_t row0; int64_t n; int d; int ld;
+    int bf16_out; int kind; uint64_t seed; uint32_t stream; int C;
+};
+
+hipError_t knn_launch_exact_scan(const ExactScanArgs& a, int grid, hipStream_t st);
+size_t knn_exact_scan_lds(int d, int k, int C);
+hipError_t knn_launch_row_norms(const float* x, int64_t n, int ld, int d, float* out,
+                                int32_t* status, hipStream_t st);
+hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int dk, hipStream_t st);
+size_t knn_gemm_filter_lds(int dk, int k);
+hipError_t knn_gemm_filter_occupancy(int dk, int k, int* blocks_per_cu);
+hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st);
+hipError_t knn_launch_generate(const GenerateArgs& a, hipStream_t st);

@@ -1,0 +1,169 @@
+"""GPU parity: the HIP path through the C ABI vs the reference's fixtures and the oracle.
+
+Bar: bit-exact predictions, top-k train indices and top-k distance bits (the reference's
+direct-form fp32 distance, main.cpp:14-23), on both device algorithms.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import (DATA, DATASETS, KS, PKG_DIR, golden_cm, golden_manifest, golden_topk,
+                      pred_sha)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctxs(knn):
+    out = {a: knn.Context(0, algo=a) for a in ("direct", "gemm", "auto")}
+    yield out
+    for c in out.values():
+        c.close()
+
+
+@pytest.fixture(scope="module")
+def arff(knn):
+    return {ds: (knn.read_arff(f"{DATA}/{ds}-train.arff"), knn.read_arff(f"{DATA}/{ds}-test.arff"))
+            for ds in DATASETS}
+
+
+@pytest.mark.parametrize("algo", ["direct", "gemm"])
+@pytest.mark.parametrize("ds", DATASETS)
+@pytest.mark.parametrize("k", KS)
+def test_arff_golden(knn, ctxs, arff, algo, ds, k):
+    (tf, tl, C), (qf, ql, Cq) = arff[ds]
+    pred, dist, idx = ctxs[algo].predict(tf, tl, qf, k, C, topk=True)
+    assert pred_sha(pred) == golden_manifest()[f"{ds}_k{k}"]["sha256"]
+    gd, gi = golden_topk(ds, k)
+    assert np.array_equal(idx, gi)
+    assert np.array_equal(dist.view(np.uint32), gd)
+    acc, cm = golden_cm(ds, k)
+    mycm = knn.computeConfusionMatrix(pred, ql, Cq)
+    assert np.array_equal(mycm, cm)
+    assert f"{knn.computeAccuracy(mycm, len(pred)):.4f}" == f"{acc:.4f}"
+
+
+def test_query_range(ctxs, arff):
+    """mpi.cpp:26 / multi-thread.cpp:37 slices == the same rows of the full run."""
+    (tf, tl, C), (qf, ql, _) = arff["large"]
+    full = ctxs["auto"].predict(tf, tl, qf, 5, C)
+    for s, e in [(0, 1), (100, 615), (1717, 1718), (0, 1718)]:
+        assert np.array_equal(ctxs["direct"].predict(tf, tl, qf, 5, C, s, e), full[s:e])
+
+
+@pytest.mark.parametrize("d,k,nt,nq", [(128, 10, 20000, 300), (64, 32, 30000, 200), (100, 5, 9000, 257),
+                                       (128, 1, 5000, 130), (40, 100, 12000, 64), (128, 128, 8192, 70)])
+def test_synthetic_vs_oracle(knn, oracle, ctxs, d, k, nt, nq):
+    tr, tl = oracle.gen(7, 0, 0, nt, d)
+    te, _ = oracle.gen(7, 1, 0, nq, d)
+    bad, opred, odist, oidx = oracle.knn(tr, tl, te, k, 10)
+    assert bad == 0
+    for algo in ("direct", "gemm"):
+        pred, dist, idx = ctxs[algo].predict(tr, tl, te, k, 10, topk=True)
+        assert np.array_equal(idx, oidx), algo
+        assert np.array_equal(dist.view(np.uint32), odist.view(np.uint32)), algo
+        assert np.array_equal(pred, opred), algo
+
+
+def test_gemm_duplicates_and_ties(knn, oracle, ctxs):
+    """Heavy exact ties (as in large-train: rows repeated up to 56x) through the GEMM path."""
+    rng = np.random.default_rng(3)
+    base = rng.integers(-3, 4, size=(50, 64)).astype(np.float32)
+    tr = base[rng.integers(0, 50, size=12000)]
+    tl = rng.integers(0, 10, size=12000).astype(np.int32)
+    te = base[rng.integers(0, 50, size=100)] + 0.5 * rng.integers(0, 2, size=(100, 64)).astype(np.float32)
+    for k in (1, 7, 64):
+        bad, opred, odist, oidx = oracle.knn(tr, tl, te, k, 10)
+        pred, dist, idx = ctxs["gemm"].predict(tr, tl, te, k, 10, topk=True)
+        assert np.array_equal(idx, oidx) and np.array_equal(pred, opred)
+
+
+def test_edge_cases(knn, ctxs):
+    tr = np.arange(12, dtype=np.float32).reshape(6, 2)
+    tl = np.array([0, 1, 2, 1, 0, 1], np.int32)
+    te = np.array([[0.5, 1.5], [10, 11]], np.float32)
+    c = ctxs["auto"]
+    # k == n_train works (main.cpp accepts it)
+    p = c.predict(tr, tl, te, 6, 3)
+    assert list(p) == [1, 1]
+    # k > n_train: the reference segfaults; the ABI reports EINVAL
+    with pytest.raises(knn.KnnError) as e:
+        c.predict(tr, tl, te, 7, 3)
+    assert e.value.status == knn.KNN_EINVAL
+    # label outside [0, C)
+    with pytest.raises(knn.KnnError) as e:
+        c.predict(tr, np.array([0, 1, 5, 1, 0, 1], np.int32), te, 3, 3)
+    assert e.value.status == knn.KNN_EINVAL
+    # non-finite distances never qualify (main.cpp:47): fewer than k finite -> ERANGE
+    bad = tr.copy()
+    bad[1:, 0] = np.inf
+    with pytest.raises(knn.KnnError) as e:
+        c.predict(bad, tl, te, 2, 3)
+    assert e.value.status == knn.KNN_ERANGE
+    assert list(c.predict(bad, tl, te, 1, 3)) == [0, 0]
+    # empty query set
+    assert c.predict(tr, tl, te[:0], 3, 3).shape == (0,)
+    # k <= 0: all-zero predictions at the Python/C++ surface (reference quirk)
+    assert list(knn.KNN((tr, tl), te, 0)) == [0, 0]
+
+
+def test_generator_matches_oracle(knn, oracle):
+    import torch
+    c = knn.Context(0)
+    for kind, d, ld in ((0, 128, 128), (0, 11, 16), (1, 256, 256)):
+        feat = torch.empty((777, ld), dtype=torch.float32, device="cuda:0")
+        lab = torch.empty(777, dtype=torch.int32, device="cuda:0")
+        c.generate(feat, lab, 1000, d, kind, 5, 1, 10)
+        of, ol = oracle.gen(5, 1, 1000, 777, d, ld, kind)
+        assert np.array_equal(feat.cpu().numpy().view(np.uint32), of.view(np.uint32))
+        assert np.array_equal(lab.cpu().numpy(), ol)
+    c.close()
+
+
+def test_cli_large_k5():
+    """The C++ drop-in (knn_cli, include/knn_arff.hpp) prints the reference's line."""
+    out_file = "/tmp/knn_cli_pred_large_k5.txt"
+    env = dict(os.environ, KNN_CLI_PRED_OUT=out_file)
+    r = subprocess.run([os.path.join(PKG_DIR, "knn_cli"), f"{DATA}/large-train.arff",
+                        f"{DATA}/large-test.arff", "5"], capture_output=True, text=True, env=env,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    line = r.stdout.strip()
+    assert line.startswith("The 5-NN classifier for 1718 test instances on 30803 train instances required ")
+    assert line.endswith("ms CPU time. Accuracy was 0.9948")
+    with open(out_file) as f:
+        assert pred_sha([int(x) for x in f.read().split()]) == golden_manifest()["large_k5"]["sha256"]
+
+
+def test_full_size_config_a_sampled(knn, oracle):
+    """BASELINE config A at full size (1M x 100k x 128, k=10) on device; 48 sampled queries
+    checked bit-exactly against the oracle on the full train set."""
+    import torch
+    nt, nq, d, k = 1_000_000, 100_000, 128, 10
+    c = knn.Context(0, algo="auto", profile=True)
+    train = torch.empty((nt, d), dtype=torch.float32, device="cuda:0")
+    labels = torch.empty(nt, dtype=torch.int32, device="cuda:0")
+    test = torch.empty((nq, d), dtype=torch.float32, device="cuda:0")
+    c.generate(train, labels, 0, d, 0, 1, 0, 10)
+    c.generate(test, None, 0, d, 0, 1, 1, 10)
+    pred = torch.empty(nq, dtype=torch.int32, device="cuda:0")
+    dist = torch.empty((nq, k), dtype=torch.float32, device="cuda:0")
+    idx = torch.empty((nq, k), dtype=torch.int32, device="cuda:0")
+    c.predict_device(train, labels, test, k, 10, pred, dist, idx)
+    st = c.stats()
+    assert st["train_segments"] >= 1  # GEMM path taken
+    p, dd, ii = pred.cpu().numpy(), dist.cpu().numpy(), idx.cpu().numpy()
+    # size-independent properties: sorted neighbour lists, valid classes
+    assert np.all(np.diff(dd.view(np.uint32).astype(np.int64), axis=1) >= 0)
+    assert p.min() >= 0 and p.max() < 10
+    qs = np.linspace(0, nq - 1, 48).astype(np.int64)
+    tr_h = train.cpu().numpy()
+    lab_h = labels.cpu().numpy()
+    te_h = test.cpu().numpy()[qs]
+    bad, opred, odist, oidx = oracle.knn(tr_h, lab_h, te_h, k, 10)
+    assert np.array_equal(ii[qs], oidx)
+    assert np.array_equal(dd[qs].view(np.uint32), odist.view(np.uint32))
+    assert np.array_equal(p[qs], opred)
+    c.close()

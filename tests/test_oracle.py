@@ -1,0 +1,100 @@
+"""Pin the CPU oracle against the reference's golden fixtures (no GPU needed).
+
+The fixtures in tests/golden/ were captured from the reference itself
+(oracle/ref_capture.cpp around /root/reference/main.cpp; tests/golden/make_golden.py).
+"""
+import numpy as np
+import pytest
+
+from conftest import (DATA, DATASETS, KS, golden_cm, golden_manifest, golden_pred, golden_topk,
+                      pred_sha)
+
+SURVEY_SHA = {  # SURVEY.md 8c, captured independently by the survey
+    ("small", 1): "4bdb894a6ac2a3cf3dd63fc6e4895afa5ce7229542f8ce6933cbd4938621ba34",
+    ("small", 3): "4bdb894a6ac2a3cf3dd63fc6e4895afa5ce7229542f8ce6933cbd4938621ba34",
+    ("small", 5): "ba5cccdce3e49a58687bccbd54330ac778f052174f963c35f0b349d34741836b",
+    ("medium", 1): "8ae4dfa098c94417a0fdff2381552bcb7cedb28c44091c99b39e93a953b694b8",
+    ("medium", 3): "c1498c4261e1cb6f4f846e35165c96d7a3852779cd368b6894b51a94aaa708ed",
+    ("medium", 5): "02698225cb205c8514bd99391eae92178d8008d3002e46a18de9ffc56df185b4",
+    ("large", 1): "64d8b3c6003641ec2467d99887a35a4fd21994499b43ecf994a85f44669a4eae",
+    ("large", 3): "fce352df8a4e2d2ed87c4b6ae5fd5dd76290652808dcd38a2e77e3b6318eb4da",
+    ("large", 5): "fce352df8a4e2d2ed87c4b6ae5fd5dd76290652808dcd38a2e77e3b6318eb4da",
+    ("large", 10): "31ec143cec2c4a4981931f16b59cb30f303a5a6e9859d8e34bf997aec5073274",
+    ("large", 32): "d909b4be6eb48f78c2a826f3f633bf7c60556394562580626fb20e3dd1896eb3",
+    ("large", 100): "25f15e3c9ce04d7b31da5b3aee4e486e6f0bfa5ba96003f5a7a885c5c56b8102",
+}
+
+
+def test_manifest_matches_survey():
+    man = golden_manifest()
+    for (ds, k), sha in SURVEY_SHA.items():
+        assert man[f"{ds}_k{k}"]["sha256"] == sha
+    for key, ent in man.items():
+        assert pred_sha(golden_pred(ent["dataset"], ent["k"])) == ent["sha256"]
+
+
+@pytest.fixture(scope="module")
+def arff(oracle):
+    out = {}
+    for ds in DATASETS:
+        tr, tl, d = oracle.read_arff(f"{DATA}/{ds}-train.arff")
+        te, ql, _ = oracle.read_arff(f"{DATA}/{ds}-test.arff")
+        out[ds] = (tr, tl, te, ql, d)
+    return out
+
+
+@pytest.mark.parametrize("ds", DATASETS)
+@pytest.mark.parametrize("k", KS)
+def test_oracle_matches_reference(oracle, arff, ds, k):
+    tr, tl, te, ql, d = arff[ds]
+    C = int(tl.max()) + 1
+    bad, pred, dist, idx = oracle.knn(tr, tl, te, k, C)
+    assert bad == 0
+    assert pred_sha(pred) == golden_manifest()[f"{ds}_k{k}"]["sha256"]
+    gd, gi = golden_topk(ds, k)
+    assert np.array_equal(dist.view(np.uint32), gd)
+    assert np.array_equal(idx, gi)
+    # confusion matrix / accuracy (main.cpp:87-112)
+    acc, cm = golden_cm(ds, k)
+    Ct = int(ql.max()) + 1
+    mycm = np.zeros((Ct, Ct), np.int32)
+    oracle.lib.oracle_confusion_matrix(oracle.p(pred), oracle.p(ql), len(pred), Ct, oracle.p(mycm))
+    assert np.array_equal(mycm, cm)
+    assert f"{oracle.lib.oracle_accuracy(oracle.p(mycm), Ct, len(pred)):.4f}" == f"{acc:.4f}"
+
+
+def test_oracle_topk_is_stable_sort(oracle):
+    """Restatement check: insertion queue == first k of a stable sort by distance."""
+    rng = np.random.default_rng(0)
+    tr = rng.integers(0, 4, size=(300, 3)).astype(np.float32)  # many exact ties
+    te = rng.integers(0, 4, size=(20, 3)).astype(np.float32)
+    lab = rng.integers(0, 5, size=300).astype(np.int32)
+    k = 17
+    bad, pred, dist, idx = oracle.knn(tr, lab, te, k, 5)
+    assert bad == 0
+    for q in range(len(te)):
+        qrow = np.ascontiguousarray(te[q])
+        dd = np.array([oracle.lib.oracle_distance(oracle.p(qrow), oracle.p(tr[t]), 3)
+                       for t in range(len(tr))], np.float32)
+        order = np.argsort(dd, kind="stable")[:k]
+        assert np.array_equal(idx[q], order)
+        counts = np.bincount(lab[order], minlength=5)
+        assert pred[q] == int(np.argmax(counts))  # argmax: first max == smallest label
+
+
+def test_oracle_generator_values(oracle):
+    f, lab = oracle.gen(1, 0, 0, 64, 128)
+    assert f.min() >= -1.0 and f.max() < 1.0
+    # every value is on the 2^-23 grid
+    assert np.all((f.astype(np.float64) * 2 ** 23) == np.round(f.astype(np.float64) * 2 ** 23))
+    assert set(np.unique(lab)) <= set(range(10))
+    f2, _ = oracle.gen(1, 0, 32, 32, 128)
+    assert np.array_equal(f[32:], f2)  # counter-based: rows are independent of the block
+    fb, _ = oracle.gen(3, 0, 0, 16, 256, kind=1)
+    assert np.all(fb * 128 == np.round(fb * 128)) and fb.min() >= -1 and fb.max() < 1
+
+
+def test_oracle_k_above_n_flags(oracle):
+    tr = np.zeros((3, 2), np.float32)
+    bad, *_ = oracle.knn(tr, np.zeros(3, np.int32), tr, 4, 1)
+    assert bad == 1
