@@ -56,6 +56,14 @@ def load_library(path=LIB_PATH):
     if not os.path.exists(path):
         raise KnnError(KNN_ENODEV, f"{path} not built: run `make -C {_HERE}` "
                                    "(or __graft_entry__.build())")
+    # The torch wheel bundles its own ROCm runtime whose libamdhip64 has the same SONAME
+    # (libamdhip64.so.7) as /opt/rocm's.  Loading torch first makes this library bind to
+    # that already-loaded runtime, so a process never holds two HIP/HSA runtimes (which
+    # leaves whichever initialises second without a device).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     P, I32, I64, F = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float
     DS = ctypes.POINTER(knn_dataset)
