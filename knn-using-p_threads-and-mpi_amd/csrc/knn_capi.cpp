@@ -56,7 +56,7 @@ struct knn_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // device workspace
-    DBuf tnorm, qnorm, gthr, cnt, cand_idx, cand_L, cand_U, fb_list, ctrl;
+    DBuf tnorm, tnp, qnorm, gthr, cnt, cand_idx, cand_L, cand_U, fb_list, ctrl;
     // host-API staging (device copies of host inputs / outputs)
     DBuf h_train, h_labels, h_test, h_pred, h_dist, h_idx;
     int32_t* ctrl_host = nullptr;  // pinned: [0] status, [1] fallback count
@@ -121,7 +121,8 @@ knn_status check_dataset(knn_ctx* c, const knn_dataset* x, const char* what, boo
 
 int choose_algo(const knn_ctx* c, int64_t nt, int64_t nq, int d, int k) {
     if (c->algo == KNN_ALGO_DIRECT) return KNN_ALGO_DIRECT;
-    bool gemm_ok = d <= 128 && k <= 128 && knn_gemm_filter_lds(d <= 32 ? 32 : d <= 64 ? 64 : 128, k) <= 160 * 1024;
+    // the LDS-DMA filter stages whole rows: d must be one of its tile widths
+    bool gemm_ok = (d == 32 || d == 64 || d == 128) && k <= 128 && knn_gemm_filter_lds(d, k) <= 160 * 1024;
     if (c->algo == KNN_ALGO_GEMM) return gemm_ok ? KNN_ALGO_GEMM : KNN_ALGO_DIRECT;
     // AUTO: the direct form wins at low d (3 VALU ops per dim, no rescore) and on small jobs
     if (gemm_ok && d >= 32 && nt >= 8192 && (double)nt * (double)nq >= 1e9) return KNN_ALGO_GEMM;
@@ -170,7 +171,7 @@ void certificate(int d, float* coef, float* eta) {
 }
 
 int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dk, int k) {
-    if (c->train_splits > 0) return c->train_splits;
+    if (c->train_splits > 0) return std::min(8, c->train_splits);
     int occ = 1;
     if (knn_gemm_filter_occupancy(dk, k, &occ) != hipSuccess || occ < 1) occ = 1;
     int64_t slots = (int64_t)occ * c->num_cus;
@@ -191,20 +192,26 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     *fell_back = false;
     const int64_t nt = tr->n, nq = te->n;
     const int d = tr->d;
-    const int dk = d <= 32 ? 32 : d <= 64 ? 64 : 128;
+    const int dk = d;
     const int cap = 64 * KNN_RESCORE_CAPW;
-    HIP_OR_FAIL(c, c->tnorm.ensure(sizeof(float) * nt));
+    HIP_OR_FAIL(c, c->tnorm.ensure(sizeof(float) * (nt + 64)));
+    HIP_OR_FAIL(c, c->tnp.ensure(sizeof(float) * (nt + 64)));
     HIP_OR_FAIL(c, c->qnorm.ensure(sizeof(float) * nq));
     HIP_OR_FAIL(c, c->gthr.ensure(sizeof(uint32_t) * nq));
-    HIP_OR_FAIL(c, c->cnt.ensure(sizeof(int32_t) * nq));
+    HIP_OR_FAIL(c, c->cnt.ensure(sizeof(int32_t) * nq * 8));
     HIP_OR_FAIL(c, c->cand_idx.ensure(sizeof(int32_t) * nq * cap));
     HIP_OR_FAIL(c, c->cand_L.ensure(sizeof(float) * nq * cap));
     HIP_OR_FAIL(c, c->cand_U.ensure(sizeof(float) * nq * cap));
     HIP_OR_FAIL(c, c->fb_list.ensure(sizeof(int32_t) * nq));
 
+    float coef, eta;
+    certificate(d, &coef, &eta);
     stage_begin(c, st, "norms");
-    HIP_OR_FAIL(c, knn_launch_row_norms((const float*)tr->feat, nt, tr->ld, d, c->tnorm.as<float>(), c->ctrl.as<int32_t>(), st));
-    HIP_OR_FAIL(c, knn_launch_row_norms((const float*)te->feat, nq, te->ld, d, c->qnorm.as<float>(), c->ctrl.as<int32_t>(), st));
+    HIP_OR_FAIL(c, knn_launch_row_norms((const float*)tr->feat, nt, tr->ld, d, c->tnorm.as<float>(),
+                                        c->ctrl.as<int32_t>(), c->ctrl.as<uint32_t>() + 2,
+                                        c->tnp.as<float>(), 1.0f - coef, st));
+    HIP_OR_FAIL(c, knn_launch_row_norms((const float*)te->feat, nq, te->ld, d, c->qnorm.as<float>(),
+                                        c->ctrl.as<int32_t>(), nullptr, nullptr, 0.0f, st));
     stage_end(c, st);
     // the certificate needs every norm < 2^125; otherwise take the exact path
     HIP_OR_FAIL(c, hipMemcpyAsync(c->ctrl_host, c->ctrl.p, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
@@ -219,7 +226,6 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     }
 
     stage_begin(c, st, "filter_init");
-    HIP_OR_FAIL(c, hipMemsetAsync(c->cnt.p, 0, sizeof(int32_t) * nq, st));
     HIP_OR_FAIL(c, hipMemsetD32Async((hipDeviceptr_t)c->gthr.p, 0xFF800000u, nq, st));  // ordered(+inf)
     stage_end(c, st);
 
@@ -230,12 +236,13 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     GemmFilterArgs g{};
     g.train = (const float*)tr->feat; g.nt = nt; g.ld_t = tr->ld;
     g.test = (const float*)te->feat; g.nq = nq; g.ld_q = te->ld; g.d = d;
-    g.tnorm = c->tnorm.as<float>(); g.qnorm = c->qnorm.as<float>();
+    g.tnorm = c->tnorm.as<float>(); g.tnp = c->tnp.as<float>(); g.qnorm = c->qnorm.as<float>();
+    g.tnmax = c->ctrl.as<uint32_t>() + 2;
     g.k = k; g.seg_len = seg_len; g.nseg = nseg; g.n_qtiles = (int)n_qtiles;
-    certificate(d, &g.coef, &g.eta);
+    g.coef = coef; g.eta = eta;
     g.gthr = c->gthr.as<uint32_t>();
     g.cnt = c->cnt.as<int32_t>(); g.cand_idx = c->cand_idx.as<int32_t>();
-    g.cand_L = c->cand_L.as<float>(); g.cand_U = c->cand_U.as<float>(); g.cap = cap;
+    g.cand_L = c->cand_L.as<float>(); g.cand_U = c->cand_U.as<float>(); g.cap = cap; g.cap_seg = cap / nseg;
     stage_begin(c, st, "gemm_filter");
     HIP_OR_FAIL(c, knn_launch_gemm_filter(g, dk, st));
     stage_end(c, st);
@@ -244,6 +251,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     r.train = (const float*)tr->feat; r.labels = tr->labels; r.ld_t = tr->ld;
     r.test = (const float*)te->feat; r.ld_q = te->ld; r.nq = nq; r.d = d; r.k = k; r.C = C;
     r.cnt = g.cnt; r.cand_idx = g.cand_idx; r.cand_L = g.cand_L; r.cand_U = g.cand_U; r.cap = cap;
+    r.nseg = nseg; r.cap_seg = g.cap_seg;
     r.pred = pred; r.topk_dist = dist; r.topk_idx = idx; r.status = c->ctrl.as<int32_t>();
     r.fb_list = c->fb_list.as<int32_t>(); r.fb_count = c->ctrl.as<int32_t>() + 1;
     stage_begin(c, st, "rescore");
@@ -301,7 +309,7 @@ knn_status knn_create(knn_ctx** out, const knn_opts* opts) {
 void knn_destroy(knn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    for (DBuf* b : {&c->tnorm, &c->qnorm, &c->gthr, &c->cnt, &c->cand_idx, &c->cand_L, &c->cand_U,
+    for (DBuf* b : {&c->tnorm, &c->tnp, &c->qnorm, &c->gthr, &c->cnt, &c->cand_idx, &c->cand_L, &c->cand_U,
                     &c->fb_list, &c->ctrl, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
                     &c->h_dist, &c->h_idx})
         b->release();
@@ -347,8 +355,8 @@ knn_status knn_predict_device(knn_ctx* c, const knn_dataset* tr, const knn_datas
     c->stats[1] = c->ctrl_host[1];
     if (c->profile >= 2 && algo == KNN_ALGO_GEMM) {
         // diagnostic only: total candidates kept by the filter
-        std::vector<int32_t> h(te->n);
-        if (hipMemcpy(h.data(), c->cnt.p, sizeof(int32_t) * te->n, hipMemcpyDeviceToHost) == hipSuccess) {
+        std::vector<int32_t> h(te->n * c->stats[2]);
+        if (hipMemcpy(h.data(), c->cnt.p, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost) == hipSuccess) {
             int64_t tot = 0;
             for (int32_t v : h) tot += v;
             c->stats[0] = tot;

@@ -9,7 +9,7 @@
 #define KNN_STATUS_GEMM_UNSAFE 4   // a row norm is too large for the GEMM certificate
 
 // candidate-list capacity per query on the GEMM path (entries = 64 * CAPW)
-#define KNN_RESCORE_CAPW 16
+#define KNN_RESCORE_CAPW 32
 
 struct ExactScanArgs {
     const float* train; const int32_t* labels; int64_t nt; int ld_t;
@@ -23,17 +23,20 @@ struct ExactScanArgs {
 struct GemmFilterArgs {
     const float* train; int64_t nt; int ld_t;
     const float* test; int64_t nq; int ld_q; int d;
-    const float* tnorm; const float* qnorm;
+    const float* tnorm; const float* tnp; const float* qnorm;  // tnorm/tnp padded with +inf to nt+64
+    const uint32_t* tnmax;  // ordered bits of max tnorm
     int k; int64_t seg_len; int nseg; int n_qtiles;
     float coef; float eta;
     uint32_t* gthr;
-    int32_t* cnt; int32_t* cand_idx; float* cand_L; float* cand_U; int cap;
+    int32_t* cnt;  // [nseg][nq] kept rows per (segment, query)
+    int32_t* cand_idx; float* cand_L; float* cand_U; int cap; int cap_seg;
 };
 
 struct RescoreArgs {
     const float* train; const int32_t* labels; int ld_t;
     const float* test; int ld_q; int64_t nq; int d; int k; int C;
     const int32_t* cnt; const int32_t* cand_idx; const float* cand_L; const float* cand_U; int cap;
+    int nseg; int cap_seg;
     int32_t* pred; float* topk_dist; int32_t* topk_idx; int32_t* status;
     int32_t* fb_list; int32_t* fb_count;
     int q_lds_bytes; int c_lds_bytes; int wave_lds_bytes;  // set by the launcher
@@ -47,7 +50,7 @@ struct GenerateArgs {
 hipError_t knn_launch_exact_scan(const ExactScanArgs& a, int grid, hipStream_t st);
 size_t knn_exact_scan_lds(int d, int k, int C);
 hipError_t knn_launch_row_norms(const float* x, int64_t n, int ld, int d, float* out,
-                                int32_t* status, hipStream_t st);
+                                int32_t* status, uint32_t* maxo, float* outp, float c1, hipStream_t st);
 hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int dk, hipStream_t st);
 size_t knn_gemm_filter_lds(int dk, int k);
 hipError_t knn_gemm_filter_occupancy(int dk, int k, int* blocks_per_cu);

@@ -243,27 +243,6 @@ __global__ __launch_bounds__(256) void k_exact_scan(ExactScanArgs a) {
     }
 }
 
-// ---------------------------------------------------------------------------------
-// k_row_norms: out[r] = sum_i x[r][i]^2 (fp32).  Flags rows whose norm is too large
-// for the GEMM form's error certificate (>= 2^125) so the host falls back.
-// ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ x, int64_t n, int ld,
-                                                   int d, float* __restrict__ out,
-                                                   int32_t* __restrict__ status) {
-    int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= n) return;
-    const float* row = x + r * ld;
-    float s = 0.0f;
-    int i = 0;
-    for (; i + 4 <= d; i += 4) {
-        float4 v = *reinterpret_cast<const float4*>(row + i);
-        s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
-    }
-    for (; i < d; i++) s = fmaf(row[i], row[i], s);
-    out[r] = s;
-    if (!(s < 0x1p125f)) atomicOr(status, KNN_STATUS_GEMM_UNSAFE);
-}
-
 // ordered uint <-> float (monotone for all non-NaN floats)
 __device__ __forceinline__ uint32_t f2o(float f) {
     uint32_t b = __float_as_uint(f);
@@ -274,35 +253,91 @@ __device__ __forceinline__ float o2f(uint32_t o) {
 }
 
 // ---------------------------------------------------------------------------------
+// k_row_norms: out[r] = sum_i x[r][i]^2 (fp32).  Flags rows whose norm is too large
+// for the GEMM form's error certificate (>= 2^125) so the host falls back, and keeps
+// the maximum norm (ordered bits, atomicMax) for the filter's conservative fast test.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ x, int64_t n, int ld,
+                                                   int d, float* __restrict__ out,
+                                                   int32_t* __restrict__ status,
+                                                   uint32_t* __restrict__ maxo,
+                                                   float* __restrict__ outp, float c1) {
+    // rows [n, n + 64) of out/outp get +inf: the GEMM filter's tile tail reads them
+    int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    float s = 0.0f;
+    if (r < n) {
+        const float* row = x + r * ld;
+        int i = 0;
+        for (; i + 4 <= d; i += 4) {
+            float4 v = *reinterpret_cast<const float4*>(row + i);
+            s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
+        }
+        for (; i < d; i++) s = fmaf(row[i], row[i], s);
+        out[r] = s;
+        if (outp) outp[r] = c1 * s;
+        if (!(s < 0x1p125f)) atomicOr(status, KNN_STATUS_GEMM_UNSAFE);
+    } else if (outp && r < n + 64) {
+        out[r] = __uint_as_float(0x7f800000u);
+        outp[r] = __uint_as_float(0x7f800000u);
+    }
+    if (maxo) {
+        float m = s;
+#pragma unroll
+        for (int j = 32; j > 0; j >>= 1) m = fmaxf(m, __shfl_xor(m, j));
+        if ((threadIdx.x & 63) == 0) atomicMax(maxo, f2o(m));
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // k_gemm_filter<DK>: GEMM-form candidate filter on FP32 MFMA.
 //
-// Block = 256 threads = 4 waves; query tile BM = 128 (32 per wave) whose B-operand
-// fragments stay in VGPRs for the whole scan; train tile BN = 64 rows staged in LDS
-// (register prefetch of tile t+1 while tile t is multiplied).  Per wave and tile:
-// 2 x (DK/2) v_mfma_f32_32x32x2_f32 give a 64(train) x 32(query) block; lane l holds
-// query j = l&31 and train rows (reg&3) + 8(reg>>2) + 4(l>>5) (+32 for the 2nd block).
+// Block = 256 threads = 4 waves, 2 blocks per CU (2 waves per SIMD, independent
+// barriers so one block's epilogue hides under the other's MFMAs).  Query tile
+// BM = 128 (32 per wave): the wave's B-operand fragments
+// (s = 4g+jj) stay in VGPRs for the whole scan.  Train tiles of BN = 64 rows are
+// copied global -> LDS by LDS-DMA (global_load_lds_dwordx4, no staging registers),
+// double-buffered with one barrier per tile (the barrier's vmcnt(0) retires the DMA
+// issued one tile earlier).  Rows keep natural k order and are padded to DK+4 floats
+// (the pad slot of each row receives a harmless duplicate) so the A-operand
+// ds_read_b128 is conflict-free; lane (j,h) reads k = 8g+4h+jj, jj = 0..3, which
+// feeds 4 k-steps paired with the query fragment qf[4g+jj] = Q[q][8g+4h+jj].
+// Per tile each wave issues 2 x DK/2 v_mfma_f32_32x32x2_f32 into accumulator set X
+// while the certified test of the PREVIOUS tile (set Y) runs in between (software
+// pipelining); lane l holds query l&31 and train rows (reg&3)+8(reg>>2)+4(l>>5)
+// (+32 for the second block).
 //
-// Certificate (DESIGN.md "GEMM-form certificate"): with s = qn+tn,
-// G = s - 2 q.t, Delta = coef*s + eta, L = G - Delta <= D <= U = G + Delta for the
-// reference's direct-form D.  A train row is kept for query q iff L <= thr_q, where
-// thr_q is the k-th smallest U among kept rows (kept in LDS, sorted) or a smaller
-// threshold published by another segment of the same query (gthr, atomicMin).
-// Every row of the exact top-k satisfies L <= D <= D_(k) <= thr_q, so is kept.
+// Certificate: with s = qn+tn, G = fma(-2, q.t, s), Delta = coef*s+eta,
+// L = G - Delta <= D <= U = G + Delta for the reference's direct-form distance D.
+// A row is kept for query q iff L <= thr_q, thr_q = the k-th smallest U among rows
+// this block kept (sorted list in LDS) or a smaller bound published by another
+// segment (gthr).  Every row of the exact top-k has L <= D <= D_(k) <= thr_q.
+// The per-value fast test y = fma(-2, q.t, (1-coef) tn) <= tf_q is a conservative
+// superset of L <= thr_q (tf_q adds 2^-16 (|thr|+qn+max tn) > the rounding gap of
+// the two formulas); a wave re-checks exactly only when some lane passes (slow path).
+// Kept rows go to this segment's slice of the query's candidate list (LDS counter).
 // ---------------------------------------------------------------------------------
 static constexpr int GF_BM = 128;
 static constexpr int GF_BN = 64;
 
+__device__ __forceinline__ float f4get(const float4& v, int i) {
+    return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+}
+
 template <int DK>
 __global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
     constexpr int STRIDE = DK + 4;          // floats per LDS tile row (pad: conflict-free b128)
-    constexpr int GROUPS = GF_BN * DK / 8;  // 8-float groups per tile
-    constexpr int GPT = GROUPS / 256;       // groups per thread
-    static_assert(GROUPS % 256 == 0, "tile groups must divide the block");
+    constexpr int TILE = GF_BN * STRIDE;
+    constexpr int NG = DK / 8;              // 8-float k-groups per row
+    constexpr int SLOTS = DK / 4 + 1;       // 16-B slots per padded LDS row
+    constexpr int DMA_INS = GF_BN * SLOTS / 64;          // 1 KiB LDS-DMA instructions per tile
+    constexpr int DMA_PER_WAVE = (DMA_INS + 3) / 4;
+    constexpr int VPG = 32 / NG;            // epilogue values interleaved per k-group
+    static_assert(GF_BN * SLOTS % 64 == 0 && 32 % NG == 0, "tile geometry");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float* tile = reinterpret_cast<float*>(smem);                 // [BN][STRIDE]
-    float* tn_s = tile + GF_BN * STRIDE;                          // [BN]
-    float* spill = tn_s + GF_BN;                                  // [4 waves][32][64]
-    float* topU = spill + 4 * 32 * 64;                            // [BM][k]
+    float* tiles = reinterpret_cast<float*>(smem);                  // [2][BN][STRIDE]
+    float* ring = tiles + 2 * TILE;                                  // [3][2][BN]: (1-c) tn, tn
+    float* topU = ring + 3 * 2 * GF_BN;                              // [BM][k]
+    int* cnt_l = reinterpret_cast<int*>(topU + GF_BM * a.k);         // [BM] kept rows (this segment)
 
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
@@ -310,182 +345,216 @@ __global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
     const int h = lane >> 5;
     const int qt = blockIdx.x % a.n_qtiles;
     const int seg = blockIdx.x / a.n_qtiles;
-    const int jl = wave * 32 + j;                     // query within the tile
+    const int jl = wave * 32 + j;
     const int64_t q = (int64_t)qt * GF_BM + jl;
     const bool qvalid = q < a.nq;
     const int64_t row_begin = (int64_t)seg * a.seg_len;
     const int64_t row_end = min(a.nt, row_begin + a.seg_len);
     const int k = a.k;
+    const float INF = __uint_as_float(0x7f800000u);
+    const float coef = a.coef, eta = a.eta, c1 = 1.0f - a.coef;
+    const float tnmax = o2f(*a.tnmax);
 
-    // topU lists start at +inf
-    for (int i = threadIdx.x; i < GF_BM * k; i += 256) topU[i] = __uint_as_float(0x7f800000u);
+    for (int i = threadIdx.x; i < GF_BM * k; i += 256) topU[i] = INF;
+    for (int i = threadIdx.x; i < 3 * 2 * GF_BN; i += 256) ring[i] = INF;
+    if (threadIdx.x < GF_BM) cnt_l[threadIdx.x] = 0;
 
-    // query fragments: qf[s] = Q[q][2s + h]
     float qf[DK / 2];
     {
         const float* qrow = a.test + (qvalid ? q : 0) * a.ld_q;
 #pragma unroll
-        for (int s = 0; s < DK / 2; s++) {
-            int c = 2 * s + h;
-            qf[s] = (qvalid && c < a.d) ? qrow[c] : 0.0f;
+        for (int g = 0; g < NG; g++) {
+            const float4 v = qvalid ? *reinterpret_cast<const float4*>(qrow + 8 * g + 4 * h)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+            qf[4 * g + 0] = v.x; qf[4 * g + 1] = v.y; qf[4 * g + 2] = v.z; qf[4 * g + 3] = v.w;
         }
     }
-    const float qn = qvalid ? a.qnorm[q] : __uint_as_float(0x7f800000u);
-    float thr = qvalid ? o2f(a.gthr[q]) : -__uint_as_float(0x7f800000u);
+    const float qn = qvalid ? a.qnorm[q] : 0.0f;
+    float thr = qvalid ? o2f(a.gthr[q]) : -INF;
     float published = thr;
-    const float coef = a.coef, eta = a.eta;
+    auto make_tf = [&](float th) -> float {
+        if (!qvalid) return -INF;
+        const float m = 0x1p-16f * (fabsf(th) + qn + tnmax);
+        return ((th - c1 * qn) + eta) + m;
+    };
+    float tf = make_tf(thr);
 
-    // register prefetch of one tile: GPT groups of 8 floats per thread
-    float4 pre[GPT][2];
-    auto load_tile = [&](int64_t r0) {
+    // LDS-DMA of one tile: slot P (16 B) of the padded image -> row P / SLOTS, slot P % SLOTS;
+    // the pad slot (SLOTS-1) gets a duplicate of slot 0.  Rows past nt read row nt-1; their
+    // ring entries are +inf (tnorm/tnp are padded with +inf), so they never pass.
+    // per-lane byte offsets of this thread's DMA slots inside a tile (row*ld + slot), fixed
+    uint32_t doff[DMA_PER_WAVE];
 #pragma unroll
-        for (int i = 0; i < GPT; i++) {
-            int gi = threadIdx.x + 256 * i;
-            int row = gi / (DK / 8);
-            int g = gi % (DK / 8);
-            int64_t t = r0 + row;
-            float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
-            if (t < row_end) {
-                const float* src = a.train + t * a.ld_t + 8 * g;
-                if (8 * g + 8 <= a.d) {
-                    v0 = *reinterpret_cast<const float4*>(src);
-                    v1 = *reinterpret_cast<const float4*>(src + 4);
-                } else {
-                    float tmp[8];
+    for (int i = 0; i < DMA_PER_WAVE; i++) {
+        const int P = (wave + 4 * i) * 64 + lane;
+        const int row = P / SLOTS, sl = P % SLOTS;
+        doff[i] = (uint32_t)(row * a.ld_t + 4 * (sl == SLOTS - 1 ? 0 : sl)) * 4u;
+    }
+    auto dma_tile = [&](int buf, int slot, int64_t r0) {
+        typedef __attribute__((address_space(3))) void lds_void;
+        typedef __attribute__((address_space(1))) const void gbl_void;
+        unsigned char* tile = reinterpret_cast<unsigned char*>(tiles + buf * TILE);
+        const bool tail = r0 + GF_BN > a.nt;  // block-uniform
+        const char* base = reinterpret_cast<const char*>(a.train + r0 * a.ld_t);
 #pragma unroll
-                    for (int e = 0; e < 8; e++) tmp[e] = (8 * g + e < a.d) ? src[e] : 0.0f;
-                    v0 = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
-                    v1 = make_float4(tmp[4], tmp[5], tmp[6], tmp[7]);
+        for (int i = 0; i < DMA_PER_WAVE; i++) {
+            const int ins = wave + 4 * i;
+            if (ins < DMA_INS) {
+                const char* src = base + doff[i];
+                if (tail) {  // rows past nt re-read row nt-1 (their ring entries are +inf)
+                    const int P = ins * 64 + lane;
+                    const int row = P / SLOTS, sl = P % SLOTS;
+                    const int64_t t = min(r0 + row, a.nt - 1);
+                    src = reinterpret_cast<const char*>(a.train + t * a.ld_t + 4 * (sl == SLOTS - 1 ? 0 : sl));
                 }
+                __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(tile + ins * 1024), 16, 0, 0);
             }
-            pre[i][0] = v0;
-            pre[i][1] = v1;
         }
-    };
-    // permuted store: within each 8-group, position 4h + jj holds k = 2jj + h
-    auto store_tile = [&](int64_t r0) {
-#pragma unroll
-        for (int i = 0; i < GPT; i++) {
-            int gi = threadIdx.x + 256 * i;
-            int row = gi / (DK / 8);
-            int g = gi % (DK / 8);
-            float4 v0 = pre[i][0], v1 = pre[i][1];
-            float* dst = tile + row * STRIDE + 8 * g;
-            *reinterpret_cast<float4*>(dst) = make_float4(v0.x, v0.z, v1.x, v1.z);
-            *reinterpret_cast<float4*>(dst + 4) = make_float4(v0.y, v0.w, v1.y, v1.w);
-        }
-        if (threadIdx.x < GF_BN) {
-            int64_t t = r0 + threadIdx.x;
-            tn_s[threadIdx.x] = (t < row_end) ? a.tnorm[t] : __uint_as_float(0x7f800000u);
-        }
+        float* rs = ring + slot * 2 * GF_BN;
+        if (wave == 2)
+            __builtin_amdgcn_global_load_lds((gbl_void*)(a.tnp + r0 + lane), (lds_void*)rs, 4, 0, 0);
+        else if (wave == 3)
+            __builtin_amdgcn_global_load_lds((gbl_void*)(a.tnorm + r0 + lane), (lds_void*)(rs + GF_BN), 4, 0, 0);
     };
 
-    const int64_t ntiles = (row_end > row_begin) ? (row_end - row_begin + GF_BN - 1) / GF_BN : 0;
-    if (ntiles > 0) load_tile(row_begin);
-    for (int64_t it = 0; it < ntiles; it++) {
-        const int64_t r0 = row_begin + it * GF_BN;
-        __syncthreads();  // every wave has finished reading the previous tile
-        store_tile(r0);
-        __syncthreads();
-        if (it + 1 < ntiles) load_tile(r0 + GF_BN);
-
-        floatx16 acc0 = {}, acc1 = {};
+    // MFMAs of one tile into X, interleaved with the fast test of the previous tile (Y)
+    auto step = [&](floatx16 (&X)[2], floatx16 (&Y)[2], int buf, int slotY) -> bool {
+        const float* tile = tiles + buf * TILE;
         const float* a0p = tile + j * STRIDE + 4 * h;
         const float* a1p = tile + (32 + j) * STRIDE + 4 * h;
+        const float* tnpY = ring + slotY * 2 * GF_BN;
+        X[0] = floatx16{};
+        X[1] = floatx16{};
+        bool any = false;
+        float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int g = 0; g < DK / 8; g++) {
-            float4 x0 = *reinterpret_cast<const float4*>(a0p + 8 * g);
-            float4 x1 = *reinterpret_cast<const float4*>(a1p + 8 * g);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0.x, qf[4 * g + 0], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(x1.x, qf[4 * g + 0], acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0.y, qf[4 * g + 1], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(x1.y, qf[4 * g + 1], acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0.z, qf[4 * g + 2], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(x1.z, qf[4 * g + 2], acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0.w, qf[4 * g + 3], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(x1.w, qf[4 * g + 3], acc1, 0, 0, 0);
-        }
-
-        // epilogue: certified filter, one bit per (block, reg)
-        uint32_t mask = 0;
+        for (int g = 0; g < NG; g++) {
+            const float4 x0 = *reinterpret_cast<const float4*>(a0p + 8 * g);
+            const float4 x1 = *reinterpret_cast<const float4*>(a1p + 8 * g);
 #pragma unroll
-        for (int rb = 0; rb < 4; rb++) {
-            float4 tA = *reinterpret_cast<const float4*>(tn_s + 8 * rb + 4 * h);
-            float4 tB = *reinterpret_cast<const float4*>(tn_s + 32 + 8 * rb + 4 * h);
-            float tnA[4] = {tA.x, tA.y, tA.z, tA.w};
-            float tnB[4] = {tB.x, tB.y, tB.z, tB.w};
+            for (int jj = 0; jj < 4; jj++) {
+                X[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(x0, jj), qf[4 * g + jj], X[0], 0, 0, 0);
+                X[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(x1, jj), qf[4 * g + jj], X[1], 0, 0, 0);
+            }
 #pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const int reg = 4 * rb + e;
-                float sA = qn + tnA[e];
-                float GA = fmaf(-2.0f, acc0[reg], sA);
-                float LA = GA - fmaf(coef, sA, eta);
-                float sB = qn + tnB[e];
-                float GB = fmaf(-2.0f, acc1[reg], sB);
-                float LB = GB - fmaf(coef, sB, eta);
-                mask |= (uint32_t)(LA <= thr) << reg;
-                mask |= (uint32_t)(LB <= thr) << (16 + reg);
+            for (int vv = 0; vv < VPG; vv++) {
+                const int v = g * VPG + vv, rb = v >> 4, reg = v & 15;
+                if ((reg & 3) == 0)
+                    t4 = *reinterpret_cast<const float4*>(tnpY + 32 * rb + 8 * (reg >> 2) + 4 * h);
+                const float y = fmaf(-2.0f, Y[rb][reg], f4get(t4, reg & 3));
+                any |= (y <= tf);
             }
         }
+        return __ballot(any) != 0ull;
+    };
 
-        if (__ballot(mask != 0)) {
-            // slow path (rare after warm-up): spill the raw dot products, then the two
-            // lanes of each query take turns appending candidates and inserting U
-            float* sp = spill + wave * 32 * 64;
+    // exact re-check of tile tp (accumulators Y) for the values whose fast test passed:
+    // a bit-mask pass, then a wave-uniform loop over the set bits (the value is picked by
+    // a select chain, so the accumulators are never indexed dynamically)
+    auto slow = [&](floatx16 (&Y)[2], int64_t tp) {
+        const int64_t r0p = row_begin + tp * GF_BN;
+        const float* tnpY = ring + (int)(tp % 3) * 2 * GF_BN;
+        const float* tnY = tnpY + GF_BN;
+        uint32_t m = 0;  // bit v = value v passed; built high to low with shift-or (no literals)
 #pragma unroll
-            for (int reg = 0; reg < 16; reg++) {
-                sp[reg * 64 + lane] = acc0[reg];
-                sp[(16 + reg) * 64 + lane] = acc1[reg];
-            }
-            float* myU = topU + jl * k;
-            for (int hh = 0; hh < 2; hh++) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                if (h == hh) {
-                    uint32_t mm = mask;
-                    while (mm) {
-                        const int b = __builtin_ctz(mm);
-                        mm &= mm - 1;
-                        const int reg = b & 15;
-                        const int row = 32 * (b >> 4) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-                        const float s = qn + tn_s[row];
-                        const float G = fmaf(-2.0f, sp[b * 64 + lane], s);
-                        const float dl = fmaf(coef, s, eta);
-                        const float L = G - dl;
-                        if (!(L <= thr)) continue;  // threshold moved since the mask was taken
+        for (int v4 = 7; v4 >= 0; v4--) {
+            const int rb = v4 >> 2, rq = v4 & 3;
+            const float4 t4 = *reinterpret_cast<const float4*>(tnpY + 32 * rb + 8 * rq + 4 * h);
+#pragma unroll
+            for (int e = 3; e >= 0; e--)
+                m = (m << 1) | (uint32_t)(fmaf(-2.0f, Y[rb][4 * rq + e], f4get(t4, e)) <= tf);
+        }
+        // the two lanes of a query take turns, so each list has one writer at a time
+        float* list = topU + jl * k;
+        for (int hh = 0; hh < 2; hh++) {
+            uint32_t mm = (h == hh) ? m : 0u;
+            while (__ballot(mm != 0u)) {
+                if (mm != 0u) {
+                    const int b = __builtin_ctz(mm);
+                    mm &= mm - 1u;
+                    float acc = Y[0][0];
+#pragma unroll
+                    for (int v = 1; v < 32; v++) acc = (b == v) ? Y[v >> 4][v & 15] : acc;
+                    const int reg = b & 15;
+                    const int row = 32 * (b >> 4) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                    const float s = qn + tnY[row];
+                    const float G = fmaf(-2.0f, acc, s);
+                    const float dl = fmaf(coef, s, eta);
+                    const float L = G - dl;
+                    const int64_t t = r0p + row;
+                    if (L <= thr && t < row_end) {
                         const float U = G + dl;
-                        const int32_t t = (int32_t)(r0 + row);
-                        const int slot = atomicAdd(&a.cnt[q], 1);
-                        if (slot < a.cap) {
-                            const int64_t o = q * (int64_t)a.cap + slot;
-                            a.cand_idx[o] = t;
+                        const int slot = cnt_l[jl];
+                        cnt_l[jl] = slot + 1;
+                        if (slot < a.cap_seg) {
+                            const int64_t o = q * (int64_t)a.cap + (int64_t)seg * a.cap_seg + slot;
+                            a.cand_idx[o] = (int32_t)t;
                             a.cand_L[o] = L;
                             a.cand_U[o] = U;
                         }
-                        if (U < myU[k - 1]) {
+                        if (U < list[k - 1]) {
                             int p = k - 1;
-                            while (p > 0 && myU[p - 1] > U) {
-                                myU[p] = myU[p - 1];
+                            while (p > 0 && list[p - 1] > U) {
+                                list[p] = list[p - 1];
                                 p--;
                             }
-                            myU[p] = U;
-                            thr = fminf(thr, myU[k - 1]);
+                            list[p] = U;
+                            thr = fminf(thr, list[k - 1]);
                         }
                     }
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            if (qvalid) thr = fminf(thr, myU[k - 1]);
-            thr = fminf(thr, __shfl_xor(thr, 32));
-            if (qvalid && h == 0 && thr < published) {
+        }
+        if (qvalid) {
+            thr = fminf(thr, list[k - 1]);
+            if (h == 0 && thr < published) {
                 atomicMin(&a.gthr[q], f2o(thr));
                 published = thr;
             }
+            tf = make_tf(thr);
         }
-        // pick up thresholds published by other segments of the same queries
-        if ((it & 15) == 15 && qvalid) thr = fminf(thr, o2f(__hip_atomic_load(&a.gthr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+    };
+
+    const int64_t ntiles = (row_end > row_begin) ? (row_end - row_begin + GF_BN - 1) / GF_BN : 0;
+    floatx16 accA[2], accB[2];
+    accA[0] = accA[1] = accB[0] = accB[1] = floatx16{};
+    __syncthreads();  // LDS init above is complete before any DMA lands
+    if (ntiles > 0) dma_tile(0, 0, row_begin);
+    auto iter = [&](floatx16 (&X)[2], floatx16 (&Y)[2], int64_t it) {
+        const int64_t r0 = row_begin + it * GF_BN;
+        if ((it & 15) == 15 && qvalid) {
+            // pick up thresholds published by other segments (no DMA in flight here)
+            const float g = o2f(__hip_atomic_load(&a.gthr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (g < thr) { thr = g; tf = make_tf(thr); }
+        }
+        __syncthreads();  // vmcnt(0): tile it landed; every wave is done with buffer (it+1)&1, slot (it+1)%3
+        if (it + 1 < ntiles) dma_tile((int)((it + 1) & 1), (int)((it + 1) % 3), r0 + GF_BN);
+        const bool any = step(X, Y, (int)(it & 1), (int)((it + 2) % 3));
+        if (any && it > 0) slow(Y, it - 1);
+    };
+    for (int64_t it = 0; it < ntiles; it += 2) {
+        iter(accA, accB, it);
+        if (it + 1 < ntiles) iter(accB, accA, it + 1);
     }
+    if (ntiles > 0) {
+        // drain: the last tile's accumulators are in accA (ntiles odd) or accB (even)
+        const int64_t last = ntiles - 1;
+        bool any = false;
+        floatx16 (&L)[2] = (last & 1) ? accB : accA;
+        const float* tnpL = ring + (int)(last % 3) * 2 * GF_BN;
+#pragma unroll
+        for (int v = 0; v < 32; v++) {
+            const int rb = v >> 4, reg = v & 15;
+            const int row = 32 * rb + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            any |= fmaf(-2.0f, L[rb][reg], tnpL[row]) <= tf;
+        }
+        if (__ballot(any)) slow(L, last);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (qvalid && h == 0) a.cnt[(int64_t)seg * a.nq + q] = cnt_l[jl];
 }
 
 // ---------------------------------------------------------------------------------
@@ -506,20 +575,27 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
     int32_t* surv = reinterpret_cast<int32_t*>(my + a.q_lds_bytes + a.c_lds_bytes);
     const int64_t q = (int64_t)blockIdx.x * 4 + wave;
     if (q >= a.nq) return;
-    const int n = a.cnt[q];
     const int k = a.k;
-    if (n > a.cap || n < k) {
+    int total = 0;
+    bool overflow = false;
+    for (int sg = 0; sg < a.nseg; sg++) {
+        const int ns = a.cnt[(int64_t)sg * a.nq + q];
+        overflow |= ns > a.cap_seg;
+        total += ns;
+    }
+    if (overflow || total < k) {
         if (lane == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = (int32_t)q;
         return;
     }
-    // load candidates (ordered-uint U, float L)
+    // load candidates (ordered-uint U, float L); entry e lives in segment e / cap_seg
     uint32_t uo[CAPW];
     float lv[CAPW];
 #pragma unroll
     for (int i = 0; i < CAPW; i++) {
-        int e = lane + 64 * i;
-        bool v = e < n;
-        int64_t o = q * (int64_t)a.cap + e;
+        const int e = lane + 64 * i;
+        const int sg = e / a.cap_seg;
+        const bool v = sg < a.nseg && (e - sg * a.cap_seg) < a.cnt[(int64_t)min(sg, a.nseg - 1) * a.nq + q];
+        const int64_t o = q * (int64_t)a.cap + e;
         uo[i] = v ? f2o(a.cand_U[o]) : 0xffffffffu;
         lv[i] = v ? a.cand_L[o] : __uint_as_float(0x7f800000u);
     }
@@ -537,7 +613,7 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
     int m = 0;
 #pragma unroll
     for (int i = 0; i < CAPW; i++) {
-        bool s = lv[i] <= thr;
+        bool s = lv[i] <= thr && uo[i] != 0xffffffffu;
         u64 bal = __ballot(s);
         if (s) {
             int pos = m + __popcll(bal & ((1ull << lane) - 1ull));
@@ -636,16 +712,18 @@ size_t knn_exact_scan_lds(int d, int k, int C) {
 }
 
 hipError_t knn_launch_row_norms(const float* x, int64_t n, int ld, int d, float* out,
-                                int32_t* status, hipStream_t st) {
+                                int32_t* status, uint32_t* maxo, float* outp, float c1, hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n, ld, d,
-                       out, status);
+    const int64_t rows = n + (outp ? 64 : 0);
+    hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, x, n, ld, d,
+                       out, status, maxo, outp, c1);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }
 
 size_t knn_gemm_filter_lds(int dk, int k) {
-    return ((size_t)GF_BN * (dk + 4) + GF_BN + 4 * 32 * 64 + (size_t)GF_BM * k) * sizeof(float);
+    return (2 * (size_t)GF_BN * (dk + 4) + 3 * 2 * GF_BN + (size_t)GF_BM * k) * sizeof(float) +
+           GF_BM * sizeof(int);
 }
 
 template <int DK>

@@ -1,0 +1,29 @@
+#!/bin/bash
+# Profile bench.py workload A on one MI355X (run on the GPU box via gpurun):
+#   1. rocprofv3 --kernel-trace --stats           -> per-kernel average durations
+#   2. rocprofv3 --pmc FETCH_SIZE                 -> HBM read bytes   (own pass)
+#   3. rocprofv3 --pmc WRITE_SIZE                 -> HBM write bytes  (own pass)
+#   4. rocprofv3 --pmc SQ_* / GRBM_GUI_ACTIVE     -> MFMA busy, clock (own pass)
+# Outputs land in gpurun_out/prof_*; scripts/summarize_profile.py turns them into
+# profiles/<tag>_*.{csv,json}.  Every pass runs under its own time limit and the chain
+# stops at the first failure.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+STEPS=${STEPS:-2}
+cd /tmp && export TMPDIR=/tmp
+OUT=$R/gpurun_out
+BENCH="$R/bench.py --steps $STEPS --warmup 1 --no-cpu-baseline"
+
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_trace -o run \
+    -- python3 $BENCH > $OUT/prof_trace.log 2>&1 || { echo "trace pass failed"; exit 1; }
+echo "trace pass ok"
+timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof_fetch -o run \
+    -- python3 $BENCH > $OUT/prof_fetch.log 2>&1 || { echo "fetch pass failed"; exit 1; }
+echo "fetch pass ok"
+timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof_write -o run \
+    -- python3 $BENCH > $OUT/prof_write.log 2>&1 || { echo "write pass failed"; exit 1; }
+echo "write pass ok"
+timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
+    --output-format csv -d $OUT/prof_sq -o run \
+    -- python3 $BENCH > $OUT/prof_sq.log 2>&1 || { echo "sq pass failed"; exit 1; }
+echo "sq pass ok"

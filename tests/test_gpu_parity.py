@@ -34,7 +34,14 @@ def arff(knn):
 @pytest.mark.parametrize("k", KS)
 def test_arff_golden(knn, ctxs, arff, algo, ds, k):
     (tf, tl, C), (qf, ql, Cq) = arff[ds]
+    if algo == "gemm":
+        # zero-pad d=7/11 to the filter's 32-wide tile: the extra (0-0)^2 terms add +0 at the
+        # end of the sequential sum, so distances stay bit-identical to the reference
+        tf = np.pad(tf, ((0, 0), (0, 32 - tf.shape[1])))
+        qf = np.pad(qf, ((0, 0), (0, 32 - qf.shape[1])))
     pred, dist, idx = ctxs[algo].predict(tf, tl, qf, k, C, topk=True)
+    if algo == "gemm":
+        assert ctxs[algo].stats()["train_segments"] >= 1  # the MFMA filter path ran
     assert pred_sha(pred) == golden_manifest()[f"{ds}_k{k}"]["sha256"]
     gd, gi = golden_topk(ds, k)
     assert np.array_equal(idx, gi)
@@ -54,7 +61,8 @@ def test_query_range(ctxs, arff):
 
 
 @pytest.mark.parametrize("d,k,nt,nq", [(128, 10, 20000, 300), (64, 32, 30000, 200), (100, 5, 9000, 257),
-                                       (128, 1, 5000, 130), (40, 100, 12000, 64), (128, 128, 8192, 70)])
+                                       (128, 1, 5000, 130), (40, 100, 12000, 64), (128, 128, 8192, 70),
+                                       (32, 3, 70001, 129), (64, 100, 20000, 100), (128, 10, 64, 5)])
 def test_synthetic_vs_oracle(knn, oracle, ctxs, d, k, nt, nq):
     tr, tl = oracle.gen(7, 0, 0, nt, d)
     te, _ = oracle.gen(7, 1, 0, nq, d)
@@ -62,6 +70,8 @@ def test_synthetic_vs_oracle(knn, oracle, ctxs, d, k, nt, nq):
     assert bad == 0
     for algo in ("direct", "gemm"):
         pred, dist, idx = ctxs[algo].predict(tr, tl, te, k, 10, topk=True)
+        if algo == "gemm" and d in (32, 64, 128):
+            assert ctxs[algo].stats()["train_segments"] >= 1
         assert np.array_equal(idx, oidx), algo
         assert np.array_equal(dist.view(np.uint32), odist.view(np.uint32)), algo
         assert np.array_equal(pred, opred), algo
@@ -77,6 +87,7 @@ def test_gemm_duplicates_and_ties(knn, oracle, ctxs):
     for k in (1, 7, 64):
         bad, opred, odist, oidx = oracle.knn(tr, tl, te, k, 10)
         pred, dist, idx = ctxs["gemm"].predict(tr, tl, te, k, 10, topk=True)
+        assert ctxs["gemm"].stats()["train_segments"] >= 1
         assert np.array_equal(idx, oidx) and np.array_equal(pred, opred)
 
 
