@@ -77,6 +77,7 @@ def main():
     ap.add_argument("--config", default="A", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--algo", default="auto", choices=["auto", "gemm", "direct"])
+    ap.add_argument("--splits", type=int, default=0, help="train segments per query tile (0 = auto)")
     args = ap.parse_args()
 
     import torch
@@ -101,7 +102,7 @@ def main():
         q0, q1 = knn.shard_range(nq_cfg, world, rank)
         nq = q1 - q0
     dev = torch.device("cuda", local)
-    ctx = knn.Context(local, algo=args.algo, profile=True)
+    ctx = knn.Context(local, algo=args.algo, train_splits=args.splits, profile=True)
     train = torch.empty((nt, d), dtype=torch.float32, device=dev)
     labels = torch.empty(nt, dtype=torch.int32, device=dev)
     test = torch.empty((nq, d), dtype=torch.float32, device=dev)

@@ -20,7 +20,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libknn_amd.so")
+# KNN_AMD_LIB overrides the library (A/B runs of alternative builds)
+LIB_PATH = os.environ.get("KNN_AMD_LIB") or os.path.join(_HERE, "libknn_amd.so")
 
 KNN_OK, KNN_EINVAL, KNN_ENOMEM, KNN_EHIP, KNN_ERANGE, KNN_ENODEV, KNN_EIO = range(7)
 STATUS_NAMES = {0: "KNN_OK", 1: "KNN_EINVAL", 2: "KNN_ENOMEM", 3: "KNN_EHIP", 4: "KNN_ERANGE",

@@ -340,7 +340,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
     int* cnt_l = reinterpret_cast<int*>(topU + GF_BM * a.k);         // [BM] kept rows (this segment)
 
     const int lane = lane_id();
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // scalar: uniform DMA branches
     const int j = lane & 31;
     const int h = lane >> 5;
     const int qt = blockIdx.x % a.n_qtiles;
@@ -441,8 +441,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
                 const int v = g * VPG + vv, rb = v >> 4, reg = v & 15;
                 if ((reg & 3) == 0)
                     t4 = *reinterpret_cast<const float4*>(tnpY + 32 * rb + 8 * (reg >> 2) + 4 * h);
+#ifndef KNN_ABLATE_NO_EPI
                 const float y = fmaf(-2.0f, Y[rb][reg], f4get(t4, reg & 3));
                 any |= (y <= tf);
+#else
+                asm volatile("" ::"v"(Y[rb][reg]), "v"(t4.x));
+#endif
             }
         }
         return __ballot(any) != 0ull;
@@ -451,9 +455,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
     // exact re-check of tile tp (accumulators Y) for the values whose fast test passed:
     // a bit-mask pass, then a wave-uniform loop over the set bits (the value is picked by
     // a select chain, so the accumulators are never indexed dynamically)
-    auto slow = [&](floatx16 (&Y)[2], int64_t tp) {
-        const int64_t r0p = row_begin + tp * GF_BN;
-        const float* tnpY = ring + (int)(tp % 3) * 2 * GF_BN;
+    auto slow = [&](floatx16 (&Y)[2], int tp) {
+        const int64_t r0p = row_begin + (int64_t)tp * GF_BN;
+        const float* tnpY = ring + (tp % 3) * 2 * GF_BN;
         const float* tnY = tnpY + GF_BN;
         uint32_t m = 0;  // bit v = value v passed; built high to low with shift-or (no literals)
 #pragma unroll
@@ -517,33 +521,39 @@ __global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
         }
     };
 
-    const int64_t ntiles = (row_end > row_begin) ? (row_end - row_begin + GF_BN - 1) / GF_BN : 0;
+    const int ntiles = (row_end > row_begin) ? (int)((row_end - row_begin + GF_BN - 1) / GF_BN) : 0;
     floatx16 accA[2], accB[2];
     accA[0] = accA[1] = accB[0] = accB[1] = floatx16{};
     __syncthreads();  // LDS init above is complete before any DMA lands
     if (ntiles > 0) dma_tile(0, 0, row_begin);
-    auto iter = [&](floatx16 (&X)[2], floatx16 (&Y)[2], int64_t it) {
-        const int64_t r0 = row_begin + it * GF_BN;
+    auto iter = [&](floatx16 (&X)[2], floatx16 (&Y)[2], int it) {
+        const int64_t r0 = row_begin + (int64_t)it * GF_BN;
         if ((it & 15) == 15 && qvalid) {
             // pick up thresholds published by other segments (no DMA in flight here)
             const float g = o2f(__hip_atomic_load(&a.gthr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             if (g < thr) { thr = g; tf = make_tf(thr); }
         }
         __syncthreads();  // vmcnt(0): tile it landed; every wave is done with buffer (it+1)&1, slot (it+1)%3
-        if (it + 1 < ntiles) dma_tile((int)((it + 1) & 1), (int)((it + 1) % 3), r0 + GF_BN);
-        const bool any = step(X, Y, (int)(it & 1), (int)((it + 2) % 3));
+#ifndef KNN_ABLATE_NO_DMA
+        if (it + 1 < ntiles) dma_tile((it + 1) & 1, (it + 1) % 3, r0 + GF_BN);
+#endif
+        const bool any = step(X, Y, it & 1, (it + 2) % 3);
+#ifndef KNN_ABLATE_NO_SLOW
         if (any && it > 0) slow(Y, it - 1);
+#else
+        if (any) asm volatile("" ::"v"(Y[0][0]), "v"(Y[1][3]));
+#endif
     };
-    for (int64_t it = 0; it < ntiles; it += 2) {
+    for (int it = 0; it < ntiles; it += 2) {
         iter(accA, accB, it);
         if (it + 1 < ntiles) iter(accB, accA, it + 1);
     }
     if (ntiles > 0) {
         // drain: the last tile's accumulators are in accA (ntiles odd) or accB (even)
-        const int64_t last = ntiles - 1;
+        const int last = ntiles - 1;
         bool any = false;
         floatx16 (&L)[2] = (last & 1) ? accB : accA;
-        const float* tnpL = ring + (int)(last % 3) * 2 * GF_BN;
+        const float* tnpL = ring + (last % 3) * 2 * GF_BN;
 #pragma unroll
         for (int v = 0; v < 32; v++) {
             const int rb = v >> 4, reg = v & 15;
