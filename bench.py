@@ -86,9 +86,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # KNN_BENCH_SHARE_GPU=1 rehearses N ranks on fewer GPUs (device = local % count, gloo);
+    # the real multi-GPU run uses one GPU per rank and RCCL ("nccl").
+    share = os.environ.get("KNN_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from importlib.util import module_from_spec, spec_from_file_location
     spec = spec_from_file_location("knn_amd", os.path.join(REPO, "knn-using-p_threads-and-mpi_amd", "__init__.py"))
@@ -96,11 +104,7 @@ def main():
     spec.loader.exec_module(knn)
 
     nt, nq_cfg, d, k, C, seed, scaling = CONFIGS[args.config]
-    if scaling == "weak":
-        q0, nq = rank * nq_cfg, nq_cfg
-    else:
-        q0, q1 = knn.shard_range(nq_cfg, world, rank)
-        nq = q1 - q0
+    q0, nq = knn.rank_queries(nq_cfg, world, rank, scaling)
     dev = torch.device("cuda", local)
     ctx = knn.Context(local, algo=args.algo, train_splits=args.splits, profile=True)
     train = torch.empty((nt, d), dtype=torch.float32, device=dev)
@@ -114,28 +118,36 @@ def main():
         ctx.predict_device(train, labels, test, k, C, pred)
         return ctx.stage_times()
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         step()
+        print(f"[bench rank {rank}] warmup {i + 1}/{args.warmup} done", file=sys.stderr, flush=True)
     stage_sum = {}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         for name, ms in step().items():
             stage_sum[name] = stage_sum.get(name, 0.0) + ms
+        if rank == 0:
+            print(f"[bench] step {i + 1}/{args.steps}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if share else dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     stats = ctx.stats()
+    total_q = nq_cfg * world if scaling == "weak" else nq_cfg
+    gathered = None
+    if world > 1:  # outside the timed region: rank 0 collects predictions (mpi.cpp:186)
+        full = knn.gather_predictions(pred.cpu().numpy(), q0, total_q, world, rank)
+        if rank == 0:
+            gathered = int((full >= 0).sum())
 
     if rank == 0:
-        total_q = nq_cfg * world if scaling == "weak" else nq_cfg
         pairs = float(total_q) * nt * args.steps
         stages = {n: v / args.steps for n, v in stage_sum.items()}
         filt_ms = stages.get("gemm_filter")
@@ -162,6 +174,7 @@ def main():
             "queries_per_s": total_q * args.steps / elapsed,
             "stages_ms": {n: round(v, 3) for n, v in stages.items()},
             "gemm_stats": stats,
+            "predictions_gathered": gathered,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -116,6 +116,32 @@ def shard_range(n, world, rank):
     return start, start + per + (left if rank == world - 1 else 0)
 
 
+def rank_queries(n_query, world, rank, scaling):
+    """Query rows [q0, q0+nq) a rank owns.  "strong": the reference's split of a fixed
+    test set (shard_range).  "weak": every rank owns n_query rows of its own,
+    rank r taking global rows [r*n_query, (r+1)*n_query)."""
+    if scaling == "weak":
+        return rank * n_query, n_query
+    q0, q1 = shard_range(n_query, world, rank)
+    return q0, q1 - q0
+
+
+def gather_predictions(pred_local, q0, n_total, world, rank, group=None):
+    """Rank 0 receives every rank's predictions at their global offsets -- the
+    reference's MPI_Gatherv (mpi.cpp:177-186) -- over torch.distributed (any backend).
+    Returns the full int32 vector on rank 0, None elsewhere."""
+    import torch.distributed as dist
+    pred_local = np.ascontiguousarray(pred_local, np.int32)
+    parts = [None] * world if rank == 0 else None
+    dist.gather_object((int(q0), pred_local), parts, dst=0, group=group)
+    if rank != 0:
+        return None
+    out = np.full(n_total, -1, np.int32)
+    for off, p in parts:
+        out[off:off + len(p)] = p
+    return out
+
+
 class Context:
     """One device, one HIP stream (knn_create / knn_destroy)."""
 

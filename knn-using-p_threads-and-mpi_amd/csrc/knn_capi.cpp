@@ -170,18 +170,24 @@ void certificate(int d, float* coef, float* eta) {
     *eta = (float)(6 * d + 8) * 0x1p-149f;
 }
 
-int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dk, int k) {
+int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dk, int k, int cap) {
     if (c->train_splits > 0) return std::min(8, c->train_splits);
     // More segments shrink the partial last wave of blocks (measured on config A:
-    // S=3 224 ms, S=5 217 ms, S=8 216 ms); each segment keeps >= 64 tiles so the
-    // per-segment threshold warm-up stays a small fraction of its scan.
+    // S=3 224 ms, S=5 217 ms, S=8 216 ms), but each segment must fit its rows in its
+    // slice of the candidate list: a running k-smallest threshold keeps about
+    // k (1 + ln(rows / k)) rows (the expected number of records) plus a 64-row warm-up
+    // tile; the slice gets a 1.5x margin.  Overflowing queries still finish exactly,
+    // on the slow full-scan fallback.
     int occ = 1;
     if (knn_gemm_filter_occupancy(dk, k, &occ) != hipSuccess || occ < 1) occ = 1;
     const int64_t slots = (int64_t)occ * c->num_cus;
     int best = 1;
     double best_eff = 0.0;
     for (int s = 1; s <= 8; s++) {
-        if (s > 1 && nt / s < 64 * 64) break;
+        const double rows = (double)nt / s;
+        if (s > 1 && rows < 64 * 64) break;
+        const double expect = k * (1.0 + std::log(std::max(rows / k, 1.0))) + 64.0;
+        if (s > 1 && 1.5 * expect > (double)(cap / s)) break;
         const int64_t w = n_qtiles * s;
         const double eff = (double)w / (double)(((w + slots - 1) / slots) * slots);
         if (eff >= best_eff) { best = s; best_eff = eff; }
@@ -232,7 +238,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     stage_end(c, st);
 
     const int64_t n_qtiles = (nq + 127) / 128;
-    const int nseg = choose_splits(c, n_qtiles, nt, dk, k);
+    const int nseg = choose_splits(c, n_qtiles, nt, dk, k, cap);
     int64_t seg_len = (nt + nseg - 1) / nseg;
     seg_len = (seg_len + 63) / 64 * 64;
     GemmFilterArgs g{};
