@@ -1,6 +1,6 @@
 """Throughput bench of the KNN hot path (BASELINE.json metric: distance pairs/s).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config A|B] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config A|B|C|C1] [--no-cpu-baseline]
 
 One process per GPU (torchrun for N > 1).  Workload A (default, BASELINE configs[2]):
 1,000,000 train x 100,000 query rows per GPU x 128-d fp32, k = 10, 10 classes, synthetic
@@ -9,6 +9,13 @@ set is sharded (rank r owns query rows [r*nq, (r+1)*nq)), train is replicated: w
 scaling with no data-path collective (the reference's MPI_Gatherv of predictions,
 mpi.cpp:186, is not part of the timed region).  A "step" is one KNN(train, test, k) pass
 over the resident inputs: norms -> MFMA filter -> exact rescore/vote -> fallback.
+
+Config C (BASELINE configs[4]) is train-sharded: 32M bf16 train rows x 1M queries x
+256-d, k = 100; rank r owns train rows shard_range(32M, N, r) and every query, computes
+the exact per-shard top-k (bf16 MFMA filter + exact fp32 rescore), the lists go through
+one all-to-all (RCCL over xGMI) to the rank that owns each query, which merges + votes.
+C1 is one rank's share of C on 8 GPUs (4M train rows x 1M queries), runnable on 1 GPU
+through the same code path.
 
 Rank 0 prints one JSON line.  roofline: the dominant kernel (k_gemm_filter) timed with
 HIP events on its own stream; cpu_baseline: the reference's pthreads KNN (oracle/_ref,
@@ -26,22 +33,28 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 CONFIGS = {
-    # name: (n_train, n_query per GPU, d, k, classes, seed, scaling)
-    "A": (1_000_000, 100_000, 128, 10, 10, 1, "weak"),
-    "B": (4_000_000, 1_000_000, 64, 32, 10, 2, "strong"),
+    # name: (n_train, n_query (per GPU when weak), d, k, classes, seed, scaling, dtype, sharding)
+    "A": (1_000_000, 100_000, 128, 10, 10, 1, "weak", "f32", "test"),
+    "B": (4_000_000, 1_000_000, 64, 32, 10, 2, "strong", "f32", "test"),
+    "C": (32_000_000, 1_000_000, 256, 100, 10, 3, "strong", "bf16", "train"),
+    "C1": (4_000_000, 1_000_000, 256, 100, 10, 3, "strong", "bf16", "train"),
 }
 METRIC = "distance pairs/sec + queries/sec at 1/2/4/8 GPUs; accuracy bit-match"
-FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+MFMA_PEAK_TFLOPS = {  # MI355X_MICROARCH.md, dense
+    "f32": 157.3,    # v_mfma_f32_32x32x2_f32
+    "bf16": 2500.0,  # v_mfma_f32_32x32x16_bf16 (~2.5 PF dense)
+}
 
 
-def cpu_baseline(d, k, C, seed):
-    """Reference pthreads KNN (multi-thread.cpp:37) on a bounded sample of workload A."""
+def cpu_baseline(d, k, C, seed, kind=0):
+    """Reference pthreads KNN (multi-thread.cpp:37) on a bounded sample of the workload."""
     threads = int(os.environ.get("KNN_BENCH_CPU_THREADS", min(16, os.cpu_count() or 1)))
-    nt_s, nq_s = 100_000, 64 * threads  # ~1e8 pairs: 10-30 s of CPU work at -O0
+    # ~1e8 pairs at d=128 (10-30 s of CPU work at -O0); fewer train rows at larger d
+    nt_s, nq_s = 100_000 * 128 // max(d, 128), 64 * threads
     exe = os.path.join(REPO, "oracle", "_ref", "ref_bench")
     sample = f"{nq_s} queries x {nt_s} train rows (d={d}, k={k}) of the same generator"
     if os.path.exists(exe):
-        out = subprocess.run([exe, "0", str(seed), str(nt_s), str(nq_s), str(d), str(k), str(C),
+        out = subprocess.run([exe, str(kind), str(seed), str(nt_s), str(nq_s), str(d), str(k), str(C),
                               str(threads)], capture_output=True, text=True, check=True, timeout=600)
         r = json.loads(out.stdout.strip().splitlines()[-1])
         return {"value": r["pairs_per_s"], "unit": "pairs/s", "cores": threads, "kind": "reference",
@@ -51,8 +64,8 @@ def cpu_baseline(d, k, C, seed):
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from conftest import Oracle
     o = Oracle()
-    tr, tl = o.gen(seed, 0, 0, nt_s, d)
-    te, _ = o.gen(seed, 1, 0, nq_s, d)
+    tr, tl = o.gen(seed, 0, 0, nt_s, d, kind=kind)
+    te, _ = o.gen(seed, 1, 0, nq_s, d, kind=kind)
     t0 = time.perf_counter()
     o.knn(tr, tl, te, k, C, threads=threads, topk=False)
     dt = time.perf_counter() - t0
@@ -60,13 +73,15 @@ def cpu_baseline(d, k, C, seed):
             "sample": sample + "; oracle/knn_oracle.c -O2", "queries_per_s": nq_s / dt}
 
 
-def pmc_traffic(round_tag=None):
-    """HBM bytes per k_gemm_filter launch from the committed rocprofv3 --pmc summary."""
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic*.json")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        return json.load(f).get("gemm_filter_bytes_per_launch")
+def pmc_traffic(config):
+    """HBM bytes per k_gemm_filter launch from the newest committed rocprofv3 --pmc
+    summary taken on this workload (profiles/*pmc_traffic*.json, key "config")."""
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic*.json")), reverse=True):
+        with open(path) as f:
+            rec = json.load(f)
+        if rec.get("config", "A") == config:
+            return rec.get("gemm_filter_bytes_per_launch")
+    return None
 
 
 def main():
@@ -103,20 +118,47 @@ def main():
     knn = module_from_spec(spec)
     spec.loader.exec_module(knn)
 
-    nt, nq_cfg, d, k, C, seed, scaling = CONFIGS[args.config]
-    q0, nq = knn.rank_queries(nq_cfg, world, rank, scaling)
+    nt, nq_cfg, d, k, C, seed, scaling, dtype, sharding = CONFIGS[args.config]
+    kind = 1 if dtype == "bf16" else 0                  # bf16-exact generator values for bf16
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
     dev = torch.device("cuda", local)
     ctx = knn.Context(local, algo=args.algo, train_splits=args.splits, profile=True)
-    train = torch.empty((nt, d), dtype=torch.float32, device=dev)
-    labels = torch.empty(nt, dtype=torch.int32, device=dev)
-    test = torch.empty((nq, d), dtype=torch.float32, device=dev)
-    ctx.generate(train, labels, 0, d, 0, seed, 0, C)   # train replicated on every rank
-    ctx.generate(test, None, q0, d, 0, seed, 1, C)     # this rank's query rows
-    pred = torch.empty(nq, dtype=torch.int32, device=dev)
+    if sharding == "test":
+        # test-sharded: train replicated on every rank, this rank's query rows
+        q0, nq = knn.rank_queries(nq_cfg, world, rank, scaling)
+        t0_row, nt_local = 0, nt
+    else:
+        # train-sharded: this rank's train rows, every query (owned queries after the exchange)
+        q0, nq = 0, nq_cfg
+        t0_row, t1_row = knn.shard_range(nt, world, rank)
+        nt_local = t1_row - t0_row
+    train = torch.empty((nt_local, d), dtype=tdt, device=dev)
+    labels = torch.empty(nt_local, dtype=torch.int32, device=dev)
+    test = torch.empty((nq, d), dtype=tdt, device=dev)
+    ctx.generate(train, labels, t0_row, d, kind, seed, 0, C)
+    ctx.generate(test, None, q0, d, kind, seed, 1, C)
+    if sharding == "test":
+        pred = torch.empty(nq, dtype=torch.int32, device=dev)
+    else:
+        rec = torch.empty((nq, 3, k), dtype=torch.int32, device=dev)
+        own0, own1 = knn.shard_range(nq, world, rank)
+        pred = torch.empty(own1 - own0, dtype=torch.int32, device=dev)
+    cur = torch.cuda.current_stream(dev).cuda_stream
 
     def step():
-        ctx.predict_device(train, labels, test, k, C, pred)
-        return ctx.stage_times()
+        if sharding == "test":
+            ctx.predict_device(train, labels, test, k, C, pred)
+            return ctx.stage_times()
+        # per-shard exact top-k -> all-to-all (RCCL) -> merge + vote, on one stream
+        ctx.shard_topk_device(train, labels, test, k, C, t0_row, rec, stream=cur)
+        times = ctx.stage_times()
+        t_x = time.perf_counter()
+        lists, _ = knn.exchange_shard_lists(rec, nq, world, rank)
+        torch.cuda.current_stream(dev).synchronize()
+        times["exchange_wall"] = 1e3 * (time.perf_counter() - t_x)
+        ctx.merge_vote_device(lists, k, C, pred, stream=cur)
+        times.update(ctx.stage_times())
+        return times
 
     for i in range(args.warmup):
         step()
@@ -143,7 +185,8 @@ def main():
     total_q = nq_cfg * world if scaling == "weak" else nq_cfg
     gathered = None
     if world > 1:  # outside the timed region: rank 0 collects predictions (mpi.cpp:186)
-        full = knn.gather_predictions(pred.cpu().numpy(), q0, total_q, world, rank)
+        p0 = q0 if sharding == "test" else own0
+        full = knn.gather_predictions(pred.cpu().numpy(), p0, total_q, world, rank)
         if rank == 0:
             gathered = int((full >= 0).sum())
 
@@ -153,24 +196,27 @@ def main():
         filt_ms = stages.get("gemm_filter")
         roof = None
         if filt_ms:
-            flops = 2.0 * d * nq * nt  # algorithmic: 2d FLOP per (query, train) pair, one launch
+            peak = MFMA_PEAK_TFLOPS[dtype]
+            flops = 2.0 * d * nq * nt_local  # algorithmic: 2d FLOP per (query, train) pair, one launch
             ach = flops / (filt_ms * 1e-3) / 1e12
-            roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
-                    "traffic": pmc_traffic(), "kernel": "k_gemm_filter",
+            roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak,
+                    "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+                    "traffic": pmc_traffic(args.config), "kernel": "k_gemm_filter",
                     "algorithmic_flops_per_launch": flops, "avg_launch_ms": round(filt_ms, 3)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(d, k, C, seed)
+            cpu = cpu_baseline(d, k, C, seed, kind)
+        par = (f"test-sharded dp{world}, train replicated" if sharding == "test" else
+               f"train-sharded x{world} (shard_range of train rows), all-to-all of per-shard top-k, merge")
         out = {
             "metric": METRIC, "value": pairs / elapsed, "unit": "pairs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
-            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": dtype,
             "data": "synthetic (counter-based generator, SURVEY.md 8d), generated in HBM",
             "config": {"workload": f"{args.config}: synthetic {nt} train x {nq_cfg} query"
-                                   f"{'/GPU' if scaling == 'weak' else ''} x {d}-d fp32, k={k}",
+                                   f"{'/GPU' if scaling == 'weak' else ''} x {d}-d {dtype}, k={k}",
                        "n_train": nt, "n_query_total": total_q, "d": d, "k": k, "classes": C,
-                       "parallelism": f"test-sharded dp{world}, train replicated"},
+                       "parallelism": par},
             "queries_per_s": total_q * args.steps / elapsed,
             "stages_ms": {n: round(v, 3) for n, v in stages.items()},
             "gemm_stats": stats,

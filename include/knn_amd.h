@@ -15,7 +15,9 @@
  *   vote      = bincount of the k labels, argmax with ties to the smallest label
  *               (main.cpp:64-78)
  * Data layout: row-major features [n][ld] (ld >= d elements, rows 16-B aligned
- * for the device entry points), int32 labels in [0, num_classes).
+ * for the device entry points), int32 labels in [0, num_classes).  Features are fp32
+ * or bf16 (KNN_BF16: raw bf16 bits; distances are the fp32 direct form on the exactly
+ * widened values, i.e. what the reference computes on those values as floats).
  */
 #ifndef KNN_AMD_H
 #define KNN_AMD_H
@@ -43,7 +45,7 @@ typedef enum { KNN_F32 = 0, KNN_BF16 = 1 } knn_dtype;
 typedef enum {
     KNN_ALGO_AUTO = 0,    /* direct form for low d / small problems, MFMA GEMM form otherwise */
     KNN_ALGO_DIRECT = 1,  /* fused direct-form distance + wave top-k + vote */
-    KNN_ALGO_GEMM = 2     /* ||q||^2+||t||^2-2q.t on FP32 MFMA + certified exact rescore */
+    KNN_ALGO_GEMM = 2     /* ||q||^2+||t||^2-2q.t on MFMA (fp32 or bf16) + certified exact rescore */
 } knn_algo;
 
 /* Context options.  One context drives one device (one HIP stream). */
@@ -101,6 +103,30 @@ knn_status knn_predict(knn_ctx* ctx, const knn_dataset* train, const knn_dataset
 knn_status knn_predict_device(knn_ctx* ctx, const knn_dataset* train, const knn_dataset* test,
                               int32_t k, int32_t num_classes, int32_t* d_pred,
                               float* d_topk_dist, int32_t* d_topk_idx, void* hip_stream);
+
+/*
+ * Train-sharded runs (the reference has only test-sharded drivers,
+ * multi-thread.cpp:154-192 / mpi.cpp:141-186, so these two calls replace the inner
+ * loop of `KNN` main.cpp:40-62 split over train shards, and its vote main.cpp:64-78).
+ *
+ * knn_shard_topk_device: the exact k nearest rows of ONE train shard for every query,
+ * written as packed int32 records d_rec[nq][3][k]: k distance bits (fp32, the
+ * reference's direct form), k global indices (idx_base + local row; -1 = none) and
+ * k labels, ascending by (distance, index).  k may exceed the shard's rows (missing
+ * entries are -1).  Device pointers; work on `hip_stream` (NULL = context stream).
+ *
+ * knn_merge_vote_device: merges nsrc such record blocks, d_rec[nsrc][nq][3][k] (e.g.
+ * after an all-to-all over the ranks that own the shards), into each query's k nearest
+ * by (distance, global index) -- the reference's tie rule over the whole train set --
+ * and votes (smallest label on ties).  d_dist / d_idx (optional) receive [nq][k].
+ * KNN_ERANGE if some query has fewer than k neighbours over all shards.
+ */
+knn_status knn_shard_topk_device(knn_ctx* ctx, const knn_dataset* train_shard, const knn_dataset* test,
+                                 int32_t k, int32_t num_classes, int64_t idx_base, int32_t* d_rec,
+                                 void* hip_stream);
+knn_status knn_merge_vote_device(knn_ctx* ctx, int32_t nsrc, int64_t nq, int32_t k, int32_t num_classes,
+                                 const int32_t* d_rec, int32_t* d_pred, float* d_dist, int32_t* d_idx,
+                                 void* hip_stream);
 
 /* Per-stage device times (ms) of the last predict call when opts.profile = 1.
  * names: optional array of n const char* to receive stage names. Returns the

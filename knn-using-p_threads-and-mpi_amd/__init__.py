@@ -10,6 +10,11 @@ Names follow the reference (srna99/KNN-using-p_threads-and-MPI):
 * ``computeAccuracy(cm, n)``                   main.cpp:102
 * ``read_arff(path)``                          libarff ArffParser::parse (arff_parser.cpp:23)
 * ``shard_range(n, world, rank)``              multi-thread.cpp:154-158 / mpi.cpp:141-170
+* ``train_sharded_predict(...)``               train-sharded KNN over ranks:
+  per-shard exact top-k -> all-to-all of neighbour lists -> merge + vote
+
+Features are fp32 or bf16.  Host bf16 arrays are numpy ``uint16`` holding bf16 bits
+(``to_bf16_bits`` / ``bf16_bits_to_f32``); device tensors are ``torch.bfloat16``.
 
 There is no CPU fallback: if ``libknn_amd.so`` is missing or no gfx950 device is
 visible, calls raise ``KnnError``.
@@ -75,6 +80,8 @@ def load_library(path=LIB_PATH):
         "knn_last_error": (ctypes.c_char_p, [P]),
         "knn_predict": (I32, [P, DS, DS, I32, I32, I64, I64, P, P, P]),
         "knn_predict_device": (I32, [P, DS, DS, I32, I32, P, P, P, P]),
+        "knn_shard_topk_device": (I32, [P, DS, DS, I32, I32, I64, P, P]),
+        "knn_merge_vote_device": (I32, [P, I32, I64, I32, I32, P, P, P, P, P]),
         "knn_stage_times": (I32, [P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(F), I32]),
         "knn_last_stats": (I32, [P, ctypes.POINTER(I64), I32]),
         "knn_generate": (I32, [P, P, P, I64, I64, I32, I32, I32, I32, ctypes.c_uint64,
@@ -98,14 +105,44 @@ def _ptr(a):
     return None if a is None else ctypes.c_void_p(a.ctypes.data)
 
 
+def to_bf16_bits(x):
+    """float32 array -> uint16 bf16 bits (round to nearest even; exact for bf16 values)."""
+    u = np.ascontiguousarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+
+
+def bf16_bits_to_f32(b):
+    """uint16 bf16 bits -> the exactly widened float32 values."""
+    return (np.ascontiguousarray(b, np.uint16).astype(np.uint32) << 16).view(np.float32)
+
+
 def _dataset(feat, labels=None):
-    feat = np.ascontiguousarray(feat, dtype=np.float32)
+    """numpy features (float32, or uint16 = bf16 bits) -> knn_dataset (+ arrays to keep alive)."""
+    if isinstance(feat, np.ndarray) and feat.dtype == np.uint16:
+        feat, dtype = np.ascontiguousarray(feat), KNN_BF16
+    else:
+        feat, dtype = np.ascontiguousarray(feat, dtype=np.float32), KNN_F32
     if feat.ndim != 2:
         raise KnnError(KNN_EINVAL, "features must be 2-D [n][d]")
     lab = None if labels is None else np.ascontiguousarray(labels, dtype=np.int32)
     ds = knn_dataset(feat.ctypes.data, None if lab is None else lab.ctypes.data, feat.shape[0],
-                     feat.shape[1], feat.shape[1], KNN_F32)
+                     feat.shape[1], feat.shape[1], dtype)
     return ds, (feat, lab)  # keep the arrays alive
+
+
+def _tensor_dtype(t):
+    import torch
+    if t.dtype == torch.bfloat16:
+        return KNN_BF16
+    if t.dtype == torch.float32:
+        return KNN_F32
+    raise KnnError(KNN_EINVAL, f"features must be float32 or bfloat16, got {t.dtype}")
+
+
+def _device_dataset(feat, labels=None, d=None):
+    d = feat.shape[1] if d is None else d
+    return knn_dataset(feat.data_ptr(), None if labels is None else labels.data_ptr(), feat.shape[0], d,
+                       feat.shape[1], _tensor_dtype(feat))
 
 
 def shard_range(n, world, rank):
@@ -140,6 +177,49 @@ def gather_predictions(pred_local, q0, n_total, world, rank, group=None):
     for off, p in parts:
         out[off:off + len(p)] = p
     return out
+
+
+def exchange_shard_lists(rec, n_query, world, rank, group=None):
+    """The train-sharded exchange: every rank holds its shard's neighbour
+    lists for ALL queries, rec [n_query][3][k]; rank r owns queries shard_range(n_query,
+    world, r) (the reference's split, mpi.cpp:141-170).  One all-to-all (RCCL over xGMI on
+    the GPU node; any torch.distributed backend works) hands each rank the lists of its
+    own queries from every shard: returns [world][nq_r][3][k] (source rank order = shard
+    order = global index order) and this rank's query range (q0, q1)."""
+    import torch
+    import torch.distributed as dist
+    k3 = rec.shape[1] * rec.shape[2]
+    spans = [shard_range(n_query, world, r) for r in range(world)]
+    q0, q1 = spans[rank]
+    send = [(b - a) * k3 for a, b in spans]          # to rank r: its query rows
+    recv = [(q1 - q0) * k3] * world                   # from every rank: my query rows
+    out = torch.empty((world, q1 - q0) + tuple(rec.shape[1:]), dtype=rec.dtype, device=rec.device)
+    if world == 1:
+        out[0].copy_(rec)
+    else:
+        dist.all_to_all_single(out.view(-1), rec.contiguous().view(-1), recv, send, group=group)
+    return out, (q0, q1)
+
+
+def train_sharded_predict(ctx, train_shard, labels_shard, idx_base, test, k, num_classes, world, rank,
+                          group=None, dist_out=None, idx_out=None, stream=None):
+    """KNN with the train set sharded over ranks: this rank's
+    shard (global rows [idx_base, idx_base + n)) against every query -> exchange ->
+    merge + vote for the queries this rank owns.  Returns (pred [nq_r] int32 device
+    tensor, (q0, q1)).  Bit-identical to the reference's serial KNN over the whole set."""
+    import torch
+    nq = test.shape[0]
+    if stream is None and test.is_cuda:
+        # one stream for topk -> all-to-all -> merge (the collective is ordered on torch's
+        # current stream, so the merge must be too)
+        stream = torch.cuda.current_stream(test.device).cuda_stream
+    rec = torch.empty((nq, 3, k), dtype=torch.int32, device=test.device)
+    ctx.shard_topk_device(train_shard, labels_shard, test, k, num_classes, idx_base, rec, stream=stream)
+    lists, (q0, q1) = exchange_shard_lists(rec, nq, world, rank, group)
+    del rec
+    pred = torch.empty(q1 - q0, dtype=torch.int32, device=test.device)
+    ctx.merge_vote_device(lists, k, num_classes, pred, dist_out, idx_out, stream=stream)
+    return pred, (q0, q1)
 
 
 class Context:
@@ -190,17 +270,39 @@ class Context:
                        stream=None, d=None):
         """Device tensors (torch, on this context's device) in and out (knn_predict_device).
         train/test: [n][ld] float32 contiguous; labels/pred/idx int32; dist float32."""
-        d = train.shape[1] if d is None else d
-        tr = knn_dataset(train.data_ptr(), labels.data_ptr(), train.shape[0], d, train.shape[1], KNN_F32)
-        te = knn_dataset(test.data_ptr(), None, test.shape[0], d, test.shape[1], KNN_F32)
+        tr = _device_dataset(train, labels, d)
+        te = _device_dataset(test, None, d)
         self._check(self.lib.knn_predict_device(
             self.h, ctypes.byref(tr), ctypes.byref(te), k, num_classes, pred.data_ptr(),
             None if dist is None else dist.data_ptr(), None if idx is None else idx.data_ptr(),
             None if stream is None else ctypes.c_void_p(stream)))
 
-    def generate(self, feat, labels, row0, d, kind, seed, stream_id, num_classes, dtype=KNN_F32,
+    def shard_topk_device(self, train, labels, test, k, num_classes, idx_base, rec, stream=None, d=None):
+        """Exact k nearest rows of one train shard for every query (knn_shard_topk_device).
+        rec: int32 device tensor [nq][3][k] <- (dist bits, idx_base + row, label), ascending."""
+        tr = _device_dataset(train, labels, d)
+        te = _device_dataset(test, None, d)
+        if tuple(rec.shape) != (test.shape[0], 3, k):
+            raise KnnError(KNN_EINVAL, f"rec must be [{test.shape[0]}, 3, {k}]")
+        self._check(self.lib.knn_shard_topk_device(
+            self.h, ctypes.byref(tr), ctypes.byref(te), k, num_classes, idx_base, rec.data_ptr(),
+            None if stream is None else ctypes.c_void_p(stream)))
+
+    def merge_vote_device(self, rec, k, num_classes, pred, dist=None, idx=None, stream=None):
+        """Merge nsrc per-shard neighbour lists rec [nsrc][nq][3][k] and vote (knn_merge_vote_device)."""
+        nsrc, nq = rec.shape[0], rec.shape[1]
+        if tuple(rec.shape[2:]) != (3, k) or pred.shape[0] != nq:
+            raise KnnError(KNN_EINVAL, "rec must be [nsrc][nq][3][k] and pred [nq]")
+        self._check(self.lib.knn_merge_vote_device(
+            self.h, nsrc, nq, k, num_classes, rec.data_ptr(), pred.data_ptr(),
+            None if dist is None else dist.data_ptr(), None if idx is None else idx.data_ptr(),
+            None if stream is None else ctypes.c_void_p(stream)))
+
+    def generate(self, feat, labels, row0, d, kind, seed, stream_id, num_classes, dtype=None,
                  stream=None):
-        """Fill a device tensor [n][ld] (and labels) with the synthetic rows of SURVEY.md 8d."""
+        """Fill a device tensor [n][ld] (and labels) with the synthetic rows of SURVEY.md 8d.
+        A bfloat16 tensor receives bf16 bits (kind 1 only: bf16-exact values)."""
+        dtype = _tensor_dtype(feat) if dtype is None else dtype
         self._check(self.lib.knn_generate(
             self.h, feat.data_ptr(), None if labels is None else labels.data_ptr(), row0,
             feat.shape[0], d, feat.shape[1], dtype, kind, seed, stream_id, num_classes,

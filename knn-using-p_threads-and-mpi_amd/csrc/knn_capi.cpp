@@ -5,6 +5,8 @@
 // become one device pipeline per context:
 //   DIRECT:  k_exact_scan                                  (fused distance/top-k/vote)
 //   GEMM:    k_row_norms x2 -> k_gemm_filter -> k_rescore -> k_exact_scan(fallback list)
+// Train-sharded runs use the same pipeline per shard with the vote
+// replaced by a packed (dist, global idx, label) neighbour list, then k_merge_vote.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -108,21 +110,27 @@ void stage_end(knn_ctx* c, hipStream_t st) {
     (void)hipEventRecord(c->stages.back().b, st);
 }
 
+int elem_size(int dtype) { return dtype == KNN_BF16 ? 2 : 4; }
+
 knn_status check_dataset(knn_ctx* c, const knn_dataset* x, const char* what, bool need_labels) {
     if (!x) return fail(c, KNN_EINVAL, "%s dataset is NULL", what);
     if (x->n < 0) return fail(c, KNN_EINVAL, "%s: n < 0", what);
     if (x->d <= 0) return fail(c, KNN_EINVAL, "%s: d must be > 0", what);
     if (x->ld < x->d) return fail(c, KNN_EINVAL, "%s: ld < d", what);
-    if (x->dtype != KNN_F32) return fail(c, KNN_EINVAL, "%s: only KNN_F32 features are supported", what);
+    if (x->dtype != KNN_F32 && x->dtype != KNN_BF16)
+        return fail(c, KNN_EINVAL, "%s: dtype must be KNN_F32 or KNN_BF16", what);
     if (x->n > 0 && !x->feat) return fail(c, KNN_EINVAL, "%s: feat is NULL", what);
     if (need_labels && x->n > 0 && !x->labels) return fail(c, KNN_EINVAL, "%s: labels are NULL", what);
     return KNN_OK;
 }
 
-int choose_algo(const knn_ctx* c, int64_t nt, int64_t nq, int d, int k) {
+int choose_algo(const knn_ctx* c, int64_t nt, int64_t nq, int d, int k, int dtype) {
     if (c->algo == KNN_ALGO_DIRECT) return KNN_ALGO_DIRECT;
-    // the LDS-DMA filter stages whole rows: d must be one of its tile widths
-    bool gemm_ok = (d == 32 || d == 64 || d == 128) && k <= 128 && knn_gemm_filter_lds(d, k) <= 160 * 1024;
+    // the LDS-DMA filter stages whole rows: a row must be one of its tile widths
+    // (128, 256 or 512 bytes: fp32 d = 32/64/128, bf16 d = 64/128/256)
+    const int rb = d * elem_size(dtype);
+    bool gemm_ok = knn_gemm_filter_supported(dtype, rb) && k <= 128 && k <= nt &&
+                   knn_gemm_filter_lds(rb, k) <= 160 * 1024;
     if (c->algo == KNN_ALGO_GEMM) return gemm_ok ? KNN_ALGO_GEMM : KNN_ALGO_DIRECT;
     // AUTO: the direct form wins at low d (3 VALU ops per dim, no rescore) and on small jobs
     if (gemm_ok && d >= 32 && nt >= 8192 && (double)nt * (double)nq >= 1e9) return KNN_ALGO_GEMM;
@@ -149,28 +157,34 @@ knn_status finish_call(knn_ctx* c, hipStream_t st) {
 }
 
 knn_status run_direct(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int k, int C,
-                      int32_t* pred, float* dist, int32_t* idx, hipStream_t st,
-                      const int32_t* qlist, const int32_t* qcount) {
+                      const QueryOut& out, hipStream_t st, const int32_t* qlist, const int32_t* qcount) {
     ExactScanArgs a{};
-    a.train = (const float*)tr->feat; a.labels = tr->labels; a.nt = tr->n; a.ld_t = tr->ld;
-    a.test = (const float*)te->feat; a.ld_q = te->ld; a.nq = te->n;
-    a.d = tr->d; a.k = k; a.C = C;
+    a.train = tr->feat; a.labels = tr->labels; a.nt = tr->n; a.ld_t = tr->ld;
+    a.test = te->feat; a.ld_q = te->ld; a.nq = te->n;
+    a.d = tr->d; a.k = k; a.C = C; a.elem = tr->dtype;
     a.qlist = qlist; a.qcount = qcount;
-    a.pred = pred; a.topk_dist = dist; a.topk_idx = idx; a.status = c->ctrl.as<int32_t>();
+    a.out = out; a.status = c->ctrl.as<int32_t>();
     int grid = qlist ? std::max(1, 2 * c->num_cus) : (int)std::min<int64_t>(te->n, 16384);
     if (grid <= 0) return KNN_OK;
     HIP_OR_FAIL(c, knn_launch_exact_scan(a, grid, st));
     return KNN_OK;
 }
 
-// GEMM-form certificate constants: Delta = coef*(qn+tn) + eta with
-// coef = (4d+32) u, eta = (6d+8) 2^-149, u = 2^-24.
-void certificate(int d, float* coef, float* eta) {
-    *coef = (float)(4 * d + 32) * 0x1p-24f;
-    *eta = (float)(6 * d + 8) * 0x1p-149f;
+// GEMM-form certificate constants: Delta = coef*(qn+tn) + eta, u = 2^-24.
+//   fp32 MFMA (an exact fmaf chain):  coef = (4d+32) u, eta = (6d+8) 2^-149
+//   bf16 MFMA (products exact; internal sums assumed no worse than 2u per add, and
+//   denormal results possibly flushed):  coef = (6d+32) u, eta = (6d+8) 2^-125
+void certificate(int d, int dtype, float* coef, float* eta) {
+    if (dtype == KNN_BF16) {
+        *coef = (float)(6 * d + 32) * 0x1p-24f;
+        *eta = (float)(6 * d + 8) * 0x1p-125f;
+    } else {
+        *coef = (float)(4 * d + 32) * 0x1p-24f;
+        *eta = (float)(6 * d + 8) * 0x1p-149f;
+    }
 }
 
-int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dk, int k, int cap) {
+int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int rb, int k, int cap) {
     if (c->train_splits > 0) return std::min(8, c->train_splits);
     // More segments shrink the partial last wave of blocks (measured on config A:
     // S=3 224 ms, S=5 217 ms, S=8 216 ms), but each segment must fit its rows in its
@@ -179,7 +193,7 @@ int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dk, int k,
     // tile; the slice gets a 1.5x margin.  Overflowing queries still finish exactly,
     // on the slow full-scan fallback.
     int occ = 1;
-    if (knn_gemm_filter_occupancy(dk, k, &occ) != hipSuccess || occ < 1) occ = 1;
+    if (knn_gemm_filter_occupancy(dtype, rb, k, &occ) != hipSuccess || occ < 1) occ = 1;
     const int64_t slots = (int64_t)occ * c->num_cus;
     int best = 1;
     double best_eff = 0.0;
@@ -196,11 +210,12 @@ int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dk, int k,
 }
 
 knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int k, int C,
-                    int32_t* pred, float* dist, int32_t* idx, hipStream_t st, bool* fell_back) {
+                    const QueryOut& out, hipStream_t st, bool* fell_back) {
     *fell_back = false;
     const int64_t nt = tr->n, nq = te->n;
     const int d = tr->d;
-    const int dk = d;
+    const int dtype = tr->dtype;
+    const int rb = d * elem_size(dtype);
     const int cap = 64 * KNN_RESCORE_CAPW;
     HIP_OR_FAIL(c, c->tnorm.ensure(sizeof(float) * (nt + 64)));
     HIP_OR_FAIL(c, c->tnp.ensure(sizeof(float) * (nt + 64)));
@@ -213,12 +228,12 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     HIP_OR_FAIL(c, c->fb_list.ensure(sizeof(int32_t) * nq));
 
     float coef, eta;
-    certificate(d, &coef, &eta);
+    certificate(d, dtype, &coef, &eta);
     stage_begin(c, st, "norms");
-    HIP_OR_FAIL(c, knn_launch_row_norms((const float*)tr->feat, nt, tr->ld, d, c->tnorm.as<float>(),
+    HIP_OR_FAIL(c, knn_launch_row_norms(tr->feat, dtype, nt, tr->ld, d, c->tnorm.as<float>(),
                                         c->ctrl.as<int32_t>(), c->ctrl.as<uint32_t>() + 2,
                                         c->tnp.as<float>(), 1.0f - coef, st));
-    HIP_OR_FAIL(c, knn_launch_row_norms((const float*)te->feat, nq, te->ld, d, c->qnorm.as<float>(),
+    HIP_OR_FAIL(c, knn_launch_row_norms(te->feat, dtype, nq, te->ld, d, c->qnorm.as<float>(),
                                         c->ctrl.as<int32_t>(), nullptr, nullptr, 0.0f, st));
     stage_end(c, st);
     // the certificate needs every norm < 2^125; otherwise take the exact path
@@ -228,7 +243,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st));
         *fell_back = true;
         stage_begin(c, st, "exact_scan");
-        knn_status s = run_direct(c, tr, te, k, C, pred, dist, idx, st, nullptr, nullptr);
+        knn_status s = run_direct(c, tr, te, k, C, out, st, nullptr, nullptr);
         stage_end(c, st);
         return s;
     }
@@ -238,12 +253,12 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     stage_end(c, st);
 
     const int64_t n_qtiles = (nq + 127) / 128;
-    const int nseg = choose_splits(c, n_qtiles, nt, dk, k, cap);
+    const int nseg = choose_splits(c, n_qtiles, nt, dtype, rb, k, cap);
     int64_t seg_len = (nt + nseg - 1) / nseg;
     seg_len = (seg_len + 63) / 64 * 64;
     GemmFilterArgs g{};
-    g.train = (const float*)tr->feat; g.nt = nt; g.ld_t = tr->ld;
-    g.test = (const float*)te->feat; g.nq = nq; g.ld_q = te->ld; g.d = d;
+    g.train = tr->feat; g.nt = nt; g.ld_t = tr->ld;
+    g.test = te->feat; g.nq = nq; g.ld_q = te->ld; g.d = d;
     g.tnorm = c->tnorm.as<float>(); g.tnp = c->tnp.as<float>(); g.qnorm = c->qnorm.as<float>();
     g.tnmax = c->ctrl.as<uint32_t>() + 2;
     g.k = k; g.seg_len = seg_len; g.nseg = nseg; g.n_qtiles = (int)n_qtiles;
@@ -252,22 +267,22 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     g.cnt = c->cnt.as<int32_t>(); g.cand_idx = c->cand_idx.as<int32_t>();
     g.cand_L = c->cand_L.as<float>(); g.cand_U = c->cand_U.as<float>(); g.cap = cap; g.cap_seg = cap / nseg;
     stage_begin(c, st, "gemm_filter");
-    HIP_OR_FAIL(c, knn_launch_gemm_filter(g, dk, st));
+    HIP_OR_FAIL(c, knn_launch_gemm_filter(g, dtype, rb, st));
     stage_end(c, st);
 
     RescoreArgs r{};
-    r.train = (const float*)tr->feat; r.labels = tr->labels; r.ld_t = tr->ld;
-    r.test = (const float*)te->feat; r.ld_q = te->ld; r.nq = nq; r.d = d; r.k = k; r.C = C;
+    r.train = tr->feat; r.labels = tr->labels; r.ld_t = tr->ld;
+    r.test = te->feat; r.ld_q = te->ld; r.nq = nq; r.d = d; r.k = k; r.C = C; r.elem = dtype;
     r.cnt = g.cnt; r.cand_idx = g.cand_idx; r.cand_L = g.cand_L; r.cand_U = g.cand_U; r.cap = cap;
     r.nseg = nseg; r.cap_seg = g.cap_seg;
-    r.pred = pred; r.topk_dist = dist; r.topk_idx = idx; r.status = c->ctrl.as<int32_t>();
+    r.out = out; r.status = c->ctrl.as<int32_t>();
     r.fb_list = c->fb_list.as<int32_t>(); r.fb_count = c->ctrl.as<int32_t>() + 1;
     stage_begin(c, st, "rescore");
     HIP_OR_FAIL(c, knn_launch_rescore(r, st));
     stage_end(c, st);
 
     stage_begin(c, st, "fallback_scan");
-    knn_status s = run_direct(c, tr, te, k, C, pred, dist, idx, st, r.fb_list, r.fb_count);
+    knn_status s = run_direct(c, tr, te, k, C, out, st, r.fb_list, r.fb_count);
     stage_end(c, st);
     c->stats[2] = nseg;
     return s;
@@ -329,34 +344,44 @@ void knn_destroy(knn_ctx* c) {
 
 const char* knn_last_error(const knn_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
-knn_status knn_predict_device(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int32_t k,
-                              int32_t C, int32_t* pred, float* dist, int32_t* idx, void* hip_stream) {
-    if (!c) return KNN_EINVAL;
-    c->err.clear();
+}  // extern "C"
+
+namespace {
+
+// Shared validation + pipeline of knn_predict_device / knn_shard_topk_device.
+// shard = true: the train set is one shard of a larger one; k may exceed its rows and
+// queries with fewer than k neighbours are not an error (the merge decides).
+knn_status predict_core(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int32_t k, int32_t C,
+                        const QueryOut& out, void* hip_stream, bool shard) {
     knn_status s;
     if ((s = check_dataset(c, tr, "train", true)) != KNN_OK) return s;
     if ((s = check_dataset(c, te, "test", false)) != KNN_OK) return s;
     if (tr->d != te->d) return fail(c, KNN_EINVAL, "feature count mismatch: train d=%d test d=%d", tr->d, te->d);
-    if (k < 1 || k > tr->n) return fail(c, KNN_EINVAL, "k=%d outside [1, n_train=%lld]", k, (long long)tr->n);
+    if (tr->dtype != te->dtype) return fail(c, KNN_EINVAL, "train and test dtypes differ");
+    if (k < 1 || (!shard && k > tr->n))
+        return fail(c, KNN_EINVAL, "k=%d outside [1, n_train=%lld]", k, (long long)tr->n);
     if (k > 1024) return fail(c, KNN_EINVAL, "k=%d exceeds the supported maximum 1024", k);
     if (C < 1 || C > 16384) return fail(c, KNN_EINVAL, "num_classes=%d outside [1, 16384]", C);
-    if (tr->n > 0x7fffffffLL) return fail(c, KNN_EINVAL, "n_train exceeds 2^31-1");
-    if ((tr->ld & 3) || (te->ld & 3) || (((uintptr_t)tr->feat) & 15) || (((uintptr_t)te->feat) & 15))
-        return fail(c, KNN_EINVAL, "device rows must be 16-byte aligned (ld %% 4 == 0)");
-    if (te->n > 0 && !pred) return fail(c, KNN_EINVAL, "pred is NULL");
+    if (tr->n + out.idx_base > 0x7fffffffLL || out.idx_base < 0)
+        return fail(c, KNN_EINVAL, "train row indices exceed 2^31-1");
+    const int es = elem_size(tr->dtype);
+    if (((int64_t)tr->ld * es) % 16 || ((int64_t)te->ld * es) % 16 || (((uintptr_t)tr->feat) & 15) ||
+        (((uintptr_t)te->feat) & 15))
+        return fail(c, KNN_EINVAL, "device rows must be 16-byte aligned (ld * element size %% 16 == 0)");
+    if (te->n > 0 && !shard && !out.pred) return fail(c, KNN_EINVAL, "pred is NULL");
     HIP_OR_FAIL(c, hipSetDevice(c->device));
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
     c->stages.clear();
     c->stats[0] = c->stats[1] = c->stats[2] = 0;
     if (te->n == 0) return KNN_OK;
     HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st));
-    int algo = choose_algo(c, tr->n, te->n, tr->d, k);
+    int algo = choose_algo(c, tr->n, te->n, tr->d, k, tr->dtype);
     if (algo == KNN_ALGO_GEMM) {
         bool fb = false;
-        if ((s = run_gemm(c, tr, te, k, C, pred, dist, idx, st, &fb)) != KNN_OK) return s;
+        if ((s = run_gemm(c, tr, te, k, C, out, st, &fb)) != KNN_OK) return s;
     } else {
         stage_begin(c, st, "exact_scan");
-        if ((s = run_direct(c, tr, te, k, C, pred, dist, idx, st, nullptr, nullptr)) != KNN_OK) return s;
+        if ((s = run_direct(c, tr, te, k, C, out, st, nullptr, nullptr)) != KNN_OK) return s;
         stage_end(c, st);
     }
     s = finish_call(c, st);
@@ -373,6 +398,51 @@ knn_status knn_predict_device(knn_ctx* c, const knn_dataset* tr, const knn_datas
     return s;
 }
 
+}  // namespace
+
+extern "C" {
+
+knn_status knn_predict_device(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int32_t k,
+                              int32_t C, int32_t* pred, float* dist, int32_t* idx, void* hip_stream) {
+    if (!c) return KNN_EINVAL;
+    c->err.clear();
+    QueryOut out{pred, dist, idx, nullptr, k, 0};
+    return predict_core(c, tr, te, k, C, out, hip_stream, false);
+}
+
+knn_status knn_shard_topk_device(knn_ctx* c, const knn_dataset* shard, const knn_dataset* te, int32_t k,
+                                 int32_t C, int64_t idx_base, int32_t* d_rec, void* hip_stream) {
+    if (!c) return KNN_EINVAL;
+    c->err.clear();
+    if (te && te->n > 0 && !d_rec) return fail(c, KNN_EINVAL, "d_rec is NULL");
+    QueryOut out{nullptr, reinterpret_cast<float*>(d_rec), d_rec ? d_rec + k : nullptr,
+                 d_rec ? d_rec + 2 * (int64_t)k : nullptr, 3 * (int64_t)k, idx_base};
+    return predict_core(c, shard, te, k, C, out, hip_stream, true);
+}
+
+knn_status knn_merge_vote_device(knn_ctx* c, int32_t nsrc, int64_t nq, int32_t k, int32_t C,
+                                 const int32_t* d_rec, int32_t* d_pred, float* d_dist, int32_t* d_idx,
+                                 void* hip_stream) {
+    if (!c) return KNN_EINVAL;
+    c->err.clear();
+    if (nsrc < 1 || nq < 0 || k < 1 || k > 1024 || C < 1 || C > 16384)
+        return fail(c, KNN_EINVAL, "merge: bad nsrc=%d nq=%lld k=%d C=%d", nsrc, (long long)nq, k, C);
+    if (nq > 0 && (!d_rec || !d_pred)) return fail(c, KNN_EINVAL, "merge: d_rec / d_pred is NULL");
+    HIP_OR_FAIL(c, hipSetDevice(c->device));
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    c->stages.clear();
+    if (nq == 0) return KNN_OK;
+    HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st));
+    MergeArgs m{};
+    m.rec = d_rec; m.nsrc = nsrc; m.nq = nq; m.k = k; m.C = C;
+    m.out = QueryOut{d_pred, d_dist, d_idx, nullptr, k, 0};
+    m.status = c->ctrl.as<int32_t>();
+    stage_begin(c, st, "merge_vote");
+    HIP_OR_FAIL(c, knn_launch_merge(m, st));
+    stage_end(c, st);
+    return finish_call(c, st);
+}
+
 knn_status knn_predict(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int32_t k, int32_t C,
                        int64_t q_begin, int64_t q_end, int32_t* out_pred, float* out_dist,
                        int32_t* out_idx) {
@@ -385,28 +455,31 @@ knn_status knn_predict(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te,
         return fail(c, KNN_EINVAL, "query range [%lld, %lld) outside [0, %lld)", (long long)q_begin,
                     (long long)q_end, (long long)te->n);
     if (tr->d != te->d) return fail(c, KNN_EINVAL, "feature count mismatch: train d=%d test d=%d", tr->d, te->d);
+    if (tr->dtype != te->dtype) return fail(c, KNN_EINVAL, "train and test dtypes differ");
     if (k < 1 || k > tr->n) return fail(c, KNN_EINVAL, "k=%d outside [1, n_train=%lld]", k, (long long)tr->n);
     const int64_t nq = q_end - q_begin;
     if (nq == 0) return KNN_OK;
     if (!out_pred) return fail(c, KNN_EINVAL, "out_pred is NULL");
     HIP_OR_FAIL(c, hipSetDevice(c->device));
     const int d = tr->d;
-    const int ldd = (d + 3) & ~3;  // device rows padded to 16 B
+    const size_t es = (size_t)elem_size(tr->dtype);
+    const int per16 = (int)(16 / es);
+    const int ldd = (d + per16 - 1) / per16 * per16;  // device rows padded to 16 B
     hipStream_t st = c->stream;
-    HIP_OR_FAIL(c, c->h_train.ensure(sizeof(float) * (size_t)ldd * tr->n));
+    HIP_OR_FAIL(c, c->h_train.ensure(es * (size_t)ldd * tr->n));
     HIP_OR_FAIL(c, c->h_labels.ensure(sizeof(int32_t) * tr->n));
-    HIP_OR_FAIL(c, c->h_test.ensure(sizeof(float) * (size_t)ldd * nq));
+    HIP_OR_FAIL(c, c->h_test.ensure(es * (size_t)ldd * nq));
     HIP_OR_FAIL(c, c->h_pred.ensure(sizeof(int32_t) * nq));
     if (out_dist) HIP_OR_FAIL(c, c->h_dist.ensure(sizeof(float) * nq * k));
     if (out_idx) HIP_OR_FAIL(c, c->h_idx.ensure(sizeof(int32_t) * nq * k));
-    HIP_OR_FAIL(c, hipMemcpy2DAsync(c->h_train.p, sizeof(float) * ldd, tr->feat, sizeof(float) * tr->ld,
-                                    sizeof(float) * d, tr->n, hipMemcpyHostToDevice, st));
+    HIP_OR_FAIL(c, hipMemcpy2DAsync(c->h_train.p, es * ldd, tr->feat, es * tr->ld, es * d, tr->n,
+                                    hipMemcpyHostToDevice, st));
     HIP_OR_FAIL(c, hipMemcpyAsync(c->h_labels.p, tr->labels, sizeof(int32_t) * tr->n, hipMemcpyHostToDevice, st));
-    HIP_OR_FAIL(c, hipMemcpy2DAsync(c->h_test.p, sizeof(float) * ldd,
-                                    (const float*)te->feat + q_begin * te->ld, sizeof(float) * te->ld,
-                                    sizeof(float) * d, nq, hipMemcpyHostToDevice, st));
-    knn_dataset dtr{c->h_train.p, c->h_labels.as<int32_t>(), tr->n, d, ldd, KNN_F32};
-    knn_dataset dte{c->h_test.p, nullptr, nq, d, ldd, KNN_F32};
+    HIP_OR_FAIL(c, hipMemcpy2DAsync(c->h_test.p, es * ldd,
+                                    (const unsigned char*)te->feat + es * (size_t)q_begin * te->ld, es * te->ld,
+                                    es * d, nq, hipMemcpyHostToDevice, st));
+    knn_dataset dtr{c->h_train.p, c->h_labels.as<int32_t>(), tr->n, d, ldd, tr->dtype};
+    knn_dataset dte{c->h_test.p, nullptr, nq, d, ldd, te->dtype};
     s = knn_predict_device(c, &dtr, &dte, k, C, c->h_pred.as<int32_t>(),
                            out_dist ? c->h_dist.as<float>() : nullptr,
                            out_idx ? c->h_idx.as<int32_t>() : nullptr, st);

@@ -11,18 +11,30 @@
 // candidate-list capacity per query on the GEMM path (entries = 64 * CAPW)
 #define KNN_RESCORE_CAPW 32
 
+// feature element types (knn_dtype): rows are fp32 or bf16 bits; every distance is the
+// reference's fp32 direct form on the (exactly) widened values
+enum { ELEM_F32 = 0, ELEM_BF16 = 1 };
+
+// Where a finished query's neighbours go.  pred may be NULL (train-shard mode: no vote);
+// dist/idx/label may be NULL; entry e of query q is at [q * stride + e]; idx is reported
+// as idx_base + local train row (train shards carry their global offset).
+struct QueryOut {
+    int32_t* pred; float* dist; int32_t* idx; int32_t* label;
+    int64_t stride; int64_t idx_base;
+};
+
 struct ExactScanArgs {
-    const float* train; const int32_t* labels; int64_t nt; int ld_t;
-    const float* test; int ld_q; int64_t nq;
-    int d; int k; int C;
+    const void* train; const int32_t* labels; int64_t nt; int ld_t;
+    const void* test; int ld_q; int64_t nq;
+    int d; int k; int C; int elem;
     const int32_t* qlist; const int32_t* qcount;  // optional query list (device count)
-    int32_t* pred; float* topk_dist; int32_t* topk_idx; int32_t* status;
+    QueryOut out; int32_t* status;
     int q_lds_bytes;                              // set by the launcher
 };
 
 struct GemmFilterArgs {
-    const float* train; int64_t nt; int ld_t;
-    const float* test; int64_t nq; int ld_q; int d;
+    const void* train; int64_t nt; int ld_t;      // ld in elements
+    const void* test; int64_t nq; int ld_q; int d;
     const float* tnorm; const float* tnp; const float* qnorm;  // tnorm/tnp padded with +inf to nt+64
     const uint32_t* tnmax;  // ordered bits of max tnorm
     int k; int64_t seg_len; int nseg; int n_qtiles;
@@ -33,13 +45,20 @@ struct GemmFilterArgs {
 };
 
 struct RescoreArgs {
-    const float* train; const int32_t* labels; int ld_t;
-    const float* test; int ld_q; int64_t nq; int d; int k; int C;
+    const void* train; const int32_t* labels; int ld_t;
+    const void* test; int ld_q; int64_t nq; int d; int k; int C; int elem;
     const int32_t* cnt; const int32_t* cand_idx; const float* cand_L; const float* cand_U; int cap;
     int nseg; int cap_seg;
-    int32_t* pred; float* topk_dist; int32_t* topk_idx; int32_t* status;
+    QueryOut out; int32_t* status;
     int32_t* fb_list; int32_t* fb_count;
     int q_lds_bytes; int c_lds_bytes; int wave_lds_bytes;  // set by the launcher
+};
+
+// Merge of per-shard neighbour lists.  rec: [nsrc][nq][3][k] int32 records (k dist bits,
+// k global indices (-1 = none), k labels), each list ascending by (dist, idx).
+struct MergeArgs {
+    const int32_t* rec; int nsrc; int64_t nq; int k; int C;
+    QueryOut out; int32_t* status;
 };
 
 struct GenerateArgs {
@@ -49,10 +68,13 @@ struct GenerateArgs {
 
 hipError_t knn_launch_exact_scan(const ExactScanArgs& a, int grid, hipStream_t st);
 size_t knn_exact_scan_lds(int d, int k, int C);
-hipError_t knn_launch_row_norms(const float* x, int64_t n, int ld, int d, float* out,
+hipError_t knn_launch_row_norms(const void* x, int elem, int64_t n, int ld, int d, float* out,
                                 int32_t* status, uint32_t* maxo, float* outp, float c1, hipStream_t st);
-hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int dk, hipStream_t st);
-size_t knn_gemm_filter_lds(int dk, int k);
-hipError_t knn_gemm_filter_occupancy(int dk, int k, int* blocks_per_cu);
+// row_bytes = d * element size: 128, 256 or 512
+bool knn_gemm_filter_supported(int elem, int row_bytes);
+hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st);
+size_t knn_gemm_filter_lds(int row_bytes, int k);
+hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks_per_cu);
 hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st);
+hipError_t knn_launch_merge(const MergeArgs& a, hipStream_t st);
 hipError_t knn_launch_generate(const GenerateArgs& a, hipStream_t st);

@@ -11,13 +11,18 @@
 // A distance that is not < FLT_MAX (inf, NaN, FLT_MAX) gets KEY_NONE and never
 // qualifies, exactly like `dist < candidates[2c]` against the FLT_MAX sentinel.
 //
+// Feature rows are fp32 or bf16 (ELEM_*).  bf16 values widen exactly to fp32, so every
+// distance is the reference's fp32 direct form on the widened values.
+//
 // Kernels
 //   k_exact_scan   fused direct-form distance + wave-resident top-k + vote (low d,
 //                  ARFF inputs, and the per-query fallback of the GEMM path)
 //   k_row_norms    ||x||^2 per row (for the GEMM form)
-//   k_gemm_filter  q.t on FP32 MFMA (v_mfma_f32_32x32x2_f32), certified candidate
-//                  filter with a running per-query threshold
+//   k_gemm_filter  q.t on MFMA (fp32: v_mfma_f32_32x32x2_f32, bf16:
+//                  v_mfma_f32_32x32x16_bf16), certified candidate filter with a
+//                  running per-query threshold
 //   k_rescore      exact direct-form rescore of the surviving candidates + top-k + vote
+//   k_merge_vote   merge of per-train-shard neighbour lists (train-sharded runs) + vote
 //   k_generate     counter-based synthetic rows (same formula as oracle/knn_oracle.c)
 #include <hip/hip_runtime.h>
 #include <float.h>
@@ -109,17 +114,35 @@ __device__ __forceinline__ u64 list_at(const u64 (&T)[R], int e) {
 }
 
 // ---------------------------------------------------------------------------------
+// Feature elements: fp32, or bf16 bits widened exactly (bf16 -> fp32 is a 16-bit shift)
+// ---------------------------------------------------------------------------------
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float widen(float v) { return v; }
+__device__ __forceinline__ float widen(bf16_t v) { return __uint_as_float((uint32_t)v << 16); }
+
+// four consecutive elements as fp32 (p aligned to 4 elements)
+__device__ __forceinline__ float4 load4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 load4(const bf16_t* p) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    return make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
+                       __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u));
+}
+
+// ---------------------------------------------------------------------------------
 // Direct-form distance, restated from main.cpp:14-23 with contraction disabled so
-// every diff*diff and += rounds to fp32 exactly like the reference.
+// every diff*diff and += rounds to fp32 exactly like the reference.  q is the query
+// row already widened to fp32 (LDS); t is a train row of element type E.
 // ---------------------------------------------------------------------------------
 #pragma clang fp contract(off)
-template <typename QP>
-__device__ __forceinline__ float direct_dist(QP q, const float* __restrict__ t, int d) {
+template <typename E>
+__device__ __forceinline__ float direct_dist(const float* q, const E* __restrict__ t, int d) {
     float sum = 0.0f;
     int i = 0;
-    if ((((uintptr_t)t) & 15) == 0) {
+    if ((((uintptr_t)t) & (4 * sizeof(E) - 1)) == 0) {
         for (; i + 4 <= d; i += 4) {
-            float4 v = *reinterpret_cast<const float4*>(t + i);
+            const float4 v = load4(t + i);
             float d0 = q[i + 0] - v.x; sum = sum + d0 * d0;
             float d1 = q[i + 1] - v.y; sum = sum + d1 * d1;
             float d2 = q[i + 2] - v.z; sum = sum + d2 * d2;
@@ -127,7 +150,7 @@ __device__ __forceinline__ float direct_dist(QP q, const float* __restrict__ t, 
         }
     }
     for (; i < d; i++) {
-        float df = q[i] - t[i];
+        float df = q[i] - widen(t[i]);
         sum = sum + df * df;
     }
     return sum;
@@ -135,38 +158,47 @@ __device__ __forceinline__ float direct_dist(QP q, const float* __restrict__ t, 
 #pragma clang fp contract(on)
 
 // ---------------------------------------------------------------------------------
-// Vote + outputs for one query from a finished wave list (main.cpp:64-78).
+// Outputs for one query from a finished wave list: the neighbour list (dist, idx_base +
+// idx, label) and, when o.pred is set, the vote of main.cpp:64-78.
 // counts: wave-private LDS array of C ints.  Runs on one wave.
 // ---------------------------------------------------------------------------------
 template <int R>
 __device__ void finish_query(const u64 (&T)[R], int k, int C, const int32_t* __restrict__ labels,
-                             int* counts, int64_t q, int32_t* __restrict__ pred,
-                             float* __restrict__ topk_dist, int32_t* __restrict__ topk_idx,
-                             int32_t* __restrict__ status) {
+                             int* counts, int64_t q, const QueryOut& o, int32_t* __restrict__ status) {
     const int lane = lane_id();
-    for (int c = lane; c < C; c += 64) counts[c] = 0;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    const bool vote = o.pred != nullptr;
+    if (vote) {
+        for (int c = lane; c < C; c += 64) counts[c] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
     u64 kth = list_at(T, k - 1);
     bool bad = (kth == KEY_NONE);
 #pragma unroll
     for (int r = 0; r < R; r++) {
         int e = 64 * r + lane;
         if (e < k) {
-            u64 key = T[r];
+            const u64 key = T[r];
+            const int64_t off = q * o.stride + e;
             if (key != KEY_NONE) {
                 int32_t idx = (int32_t)(uint32_t)(key & 0xffffffffull);
-                if (topk_dist) topk_dist[q * k + e] = __uint_as_float((uint32_t)(key >> 32));
-                if (topk_idx) topk_idx[q * k + e] = idx;
                 int lab = labels[idx];
-                if (lab >= 0 && lab < C) atomicAdd(&counts[lab], 1);
-                else atomicOr(status, KNN_STATUS_BAD_LABEL);
+                if (o.dist) o.dist[off] = __uint_as_float((uint32_t)(key >> 32));
+                if (o.idx) o.idx[off] = (int32_t)(o.idx_base + idx);
+                if (o.label) o.label[off] = lab;
+                if (lab >= 0 && lab < C) {
+                    if (vote) atomicAdd(&counts[lab], 1);
+                } else {
+                    atomicOr(status, KNN_STATUS_BAD_LABEL);
+                }
             } else {
-                if (topk_dist) topk_dist[q * k + e] = FLT_MAX;
-                if (topk_idx) topk_idx[q * k + e] = -1;
+                if (o.dist) o.dist[off] = FLT_MAX;
+                if (o.idx) o.idx[off] = -1;
+                if (o.label) o.label[off] = -1;
             }
         }
     }
+    if (!vote) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
     // argmax, strict '>' scanning 0..C-1 == max count, smallest label on ties
@@ -178,7 +210,7 @@ __device__ void finish_query(const u64 (&T)[R], int k, int C, const int32_t* __r
 #pragma unroll
     for (int j = 32; j > 0; j >>= 1) best = umax64(best, __shfl_xor(best, j));
     if (lane == 0) {
-        pred[q] = bad ? 0 : (int32_t)(0xffffffffu - (uint32_t)(best & 0xffffffffull));
+        o.pred[q] = bad ? 0 : (int32_t)(0xffffffffu - (uint32_t)(best & 0xffffffffull));
         if (bad) atomicOr(status, KNN_STATUS_TOO_FEW);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -192,7 +224,7 @@ __device__ void finish_query(const u64 (&T)[R], int k, int C, const int32_t* __r
 // into the wave list.  The four wave lists are then merged by wave 0, which votes.
 // LDS: q row [ld_pad] f32 | 4 wave lists [4][64R] u64 | counts [C] i32
 // ---------------------------------------------------------------------------------
-template <int R>
+template <int R, typename E>
 __global__ __launch_bounds__(256) void k_exact_scan(ExactScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* qs = reinterpret_cast<float*>(smem);
@@ -201,11 +233,13 @@ __global__ __launch_bounds__(256) void k_exact_scan(ExactScanArgs a) {
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     const int64_t n_work = a.qlist ? (int64_t)(*a.qcount) : a.nq;
+    const E* train = reinterpret_cast<const E*>(a.train);
+    const E* test = reinterpret_cast<const E*>(a.test);
 
     for (int64_t w = blockIdx.x; w < n_work; w += gridDim.x) {
         const int64_t q = a.qlist ? (int64_t)a.qlist[w] : w;
         __syncthreads();
-        for (int i = threadIdx.x; i < a.d; i += 256) qs[i] = a.test[q * a.ld_q + i];
+        for (int i = threadIdx.x; i < a.d; i += 256) qs[i] = widen(test[q * a.ld_q + i]);
         __syncthreads();
 
         u64 T[R];
@@ -215,7 +249,7 @@ __global__ __launch_bounds__(256) void k_exact_scan(ExactScanArgs a) {
         for (int64_t base = (int64_t)wave * 64; base < a.nt; base += 256) {
             const int64_t t = base + lane;
             u64 key = KEY_NONE;
-            if (t < a.nt) key = make_key(direct_dist(qs, a.train + t * a.ld_t, a.d), (uint32_t)t);
+            if (t < a.nt) key = make_key(direct_dist(qs, train + t * a.ld_t, a.d), (uint32_t)t);
             bool pass = key < thr;
             if (__ballot(pass)) {
                 topk_merge<R>(T, pass ? key : KEY_NONE);
@@ -237,8 +271,7 @@ __global__ __launch_bounds__(256) void k_exact_scan(ExactScanArgs a) {
                     }
                 }
             }
-            finish_query<R>(T, a.k, a.C, a.labels, counts, q, a.pred, a.topk_dist, a.topk_idx,
-                            a.status);
+            finish_query<R>(T, a.k, a.C, a.labels, counts, q, a.out, a.status);
         }
     }
 }
@@ -257,7 +290,8 @@ __device__ __forceinline__ float o2f(uint32_t o) {
 // for the GEMM form's error certificate (>= 2^125) so the host falls back, and keeps
 // the maximum norm (ordered bits, atomicMax) for the filter's conservative fast test.
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ x, int64_t n, int ld,
+template <typename E>
+__global__ __launch_bounds__(256) void k_row_norms(const E* __restrict__ x, int64_t n, int ld,
                                                    int d, float* __restrict__ out,
                                                    int32_t* __restrict__ status,
                                                    uint32_t* __restrict__ maxo,
@@ -266,13 +300,16 @@ __global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ x, 
     int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
     float s = 0.0f;
     if (r < n) {
-        const float* row = x + r * ld;
+        const E* row = x + r * ld;
         int i = 0;
         for (; i + 4 <= d; i += 4) {
-            float4 v = *reinterpret_cast<const float4*>(row + i);
+            const float4 v = load4(row + i);
             s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
         }
-        for (; i < d; i++) s = fmaf(row[i], row[i], s);
+        for (; i < d; i++) {
+            const float v = widen(row[i]);
+            s = fmaf(v, v, s);
+        }
         out[r] = s;
         if (outp) outp[r] = c1 * s;
         if (!(s < 0x1p125f)) atomicOr(status, KNN_STATUS_GEMM_UNSAFE);
@@ -289,25 +326,27 @@ __global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ x, 
 }
 
 // ---------------------------------------------------------------------------------
-// k_gemm_filter<DK>: GEMM-form candidate filter on FP32 MFMA.
+// k_gemm_filter<E, RB>: GEMM-form candidate filter on MFMA.  E = float (RB/4-d rows,
+// v_mfma_f32_32x32x2_f32, exact fp32) or bf16 (RB/2-d rows, v_mfma_f32_32x32x16_bf16);
+// RB = bytes per row (128, 256, 512).
 //
-// Block = 256 threads = 4 waves, 2 blocks per CU (2 waves per SIMD, independent
-// barriers so one block's epilogue hides under the other's MFMAs).  Query tile
-// BM = 128 (32 per wave): the wave's B-operand fragments
-// (s = 4g+jj) stay in VGPRs for the whole scan.  Train tiles of BN = 64 rows are
+// Block = 256 threads = 4 waves.  Query tile BM = 128 (32 per wave): each lane keeps
+// 16 bytes of its query row per k-step s (bytes [32s+16h, 32s+16h+16), h = lane>>5) as
+// the B-operand fragment, in VGPRs for the whole scan.  Train tiles of BN = 64 rows are
 // copied global -> LDS by LDS-DMA (global_load_lds_dwordx4, no staging registers),
 // double-buffered with one barrier per tile (the barrier's vmcnt(0) retires the DMA
-// issued one tile earlier).  Rows keep natural k order and are padded to DK+4 floats
+// issued one tile earlier).  Rows keep natural k order and are padded to RB+16 bytes
 // (the pad slot of each row receives a harmless duplicate) so the A-operand
-// ds_read_b128 is conflict-free; lane (j,h) reads k = 8g+4h+jj, jj = 0..3, which
-// feeds 4 k-steps paired with the query fragment qf[4g+jj] = Q[q][8g+4h+jj].
-// Per tile each wave issues 2 x DK/2 v_mfma_f32_32x32x2_f32 into accumulator set X
-// while the certified test of the PREVIOUS tile (set Y) runs in between (software
-// pipelining); lane l holds query l&31 and train rows (reg&3)+8(reg>>2)+4(l>>5)
-// (+32 for the second block).
+// ds_read_b128 is conflict-free; lane (j,h) reads the same 16 bytes of train rows j and
+// 32+j as its query fragment: fp32 feeds 4 k-steps of 32x32x2 (k = 8s+4h+jj), bf16 one
+// 32x32x16 (k = 16s+8h+jj, the gfx950 A/B lane map).  Per tile each wave issues the
+// MFMAs of a 64 (train) x 32 (query) block into accumulator set X while the certified
+// test of the PREVIOUS tile (set Y) runs in between (software pipelining); lane l holds
+// query l&31 and train rows (reg&3)+8(reg>>2)+4(l>>5) (+32 for the second block).
 //
 // Certificate: with s = qn+tn, G = fma(-2, q.t, s), Delta = coef*s+eta,
-// L = G - Delta <= D <= U = G + Delta for the reference's direct-form distance D.
+// L = G - Delta <= D <= U = G + Delta for the reference's direct-form distance D
+// (coef/eta per element type, set by the host).
 // A row is kept for query q iff L <= thr_q, thr_q = the k-th smallest U among rows
 // this block kept (sorted list in LDS) or a smaller bound published by another
 // segment (gthr).  Every row of the exact top-k has L <= D <= D_(k) <= thr_q.
@@ -322,20 +361,24 @@ static constexpr int GF_BN = 64;
 __device__ __forceinline__ float f4get(const float4& v, int i) {
     return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
 }
+__device__ __forceinline__ float u4getf(const uint4& v, int i) {
+    return __uint_as_float(i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w);
+}
 
-template <int DK>
+template <typename E, int RB>
 __global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
-    constexpr int STRIDE = DK + 4;          // floats per LDS tile row (pad: conflict-free b128)
+    constexpr bool BF = sizeof(E) == 2;
+    constexpr int STRIDE = RB + 16;          // bytes per LDS tile row (pad: conflict-free b128)
     constexpr int TILE = GF_BN * STRIDE;
-    constexpr int NG = DK / 8;              // 8-float k-groups per row
-    constexpr int SLOTS = DK / 4 + 1;       // 16-B slots per padded LDS row
+    constexpr int NS = RB / 32;              // k-steps: 16 B per lane half per step
+    constexpr int SLOTS = RB / 16 + 1;       // 16-B slots per padded LDS row
     constexpr int DMA_INS = GF_BN * SLOTS / 64;          // 1 KiB LDS-DMA instructions per tile
     constexpr int DMA_PER_WAVE = (DMA_INS + 3) / 4;
-    constexpr int VPG = 32 / NG;            // epilogue values interleaved per k-group
-    static_assert(GF_BN * SLOTS % 64 == 0 && 32 % NG == 0, "tile geometry");
+    constexpr int VPG = 32 / NS;             // epilogue values interleaved per k-step
+    static_assert(GF_BN * SLOTS % 64 == 0 && 32 % NS == 0, "tile geometry");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float* tiles = reinterpret_cast<float*>(smem);                  // [2][BN][STRIDE]
-    float* ring = tiles + 2 * TILE;                                  // [3][2][BN]: (1-c) tn, tn
+    unsigned char* tiles = smem;                                     // [2][BN][STRIDE]
+    float* ring = reinterpret_cast<float*>(smem + 2 * TILE);         // [3][2][BN]: (1-c) tn, tn
     float* topU = ring + 3 * 2 * GF_BN;                              // [BM][k]
     int* cnt_l = reinterpret_cast<int*>(topU + GF_BM * a.k);         // [BM] kept rows (this segment)
 
@@ -354,20 +397,20 @@ __global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
     const float INF = __uint_as_float(0x7f800000u);
     const float coef = a.coef, eta = a.eta, c1 = 1.0f - a.coef;
     const float tnmax = o2f(*a.tnmax);
+    const int64_t ldb = (int64_t)a.ld_t * sizeof(E);  // train row pitch, bytes
+    const unsigned char* trainb = reinterpret_cast<const unsigned char*>(a.train);
 
     for (int i = threadIdx.x; i < GF_BM * k; i += 256) topU[i] = INF;
     for (int i = threadIdx.x; i < 3 * 2 * GF_BN; i += 256) ring[i] = INF;
     if (threadIdx.x < GF_BM) cnt_l[threadIdx.x] = 0;
 
-    float qf[DK / 2];
+    uint4 qf[NS];
     {
-        const float* qrow = a.test + (qvalid ? q : 0) * a.ld_q;
+        const unsigned char* qrow = reinterpret_cast<const unsigned char*>(a.test) +
+                                    (qvalid ? q : 0) * (int64_t)a.ld_q * (int64_t)sizeof(E);
 #pragma unroll
-        for (int g = 0; g < NG; g++) {
-            const float4 v = qvalid ? *reinterpret_cast<const float4*>(qrow + 8 * g + 4 * h)
-                                    : make_float4(0.f, 0.f, 0.f, 0.f);
-            qf[4 * g + 0] = v.x; qf[4 * g + 1] = v.y; qf[4 * g + 2] = v.z; qf[4 * g + 3] = v.w;
-        }
+        for (int s = 0; s < NS; s++)
+            qf[s] = qvalid ? *reinterpret_cast<const uint4*>(qrow + 32 * s + 16 * h) : make_uint4(0u, 0u, 0u, 0u);
     }
     const float qn = qvalid ? a.qnorm[q] : 0.0f;
     float thr = qvalid ? o2f(a.gthr[q]) : -INF;
@@ -382,30 +425,30 @@ __global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
     // LDS-DMA of one tile: slot P (16 B) of the padded image -> row P / SLOTS, slot P % SLOTS;
     // the pad slot (SLOTS-1) gets a duplicate of slot 0.  Rows past nt read row nt-1; their
     // ring entries are +inf (tnorm/tnp are padded with +inf), so they never pass.
-    // per-lane byte offsets of this thread's DMA slots inside a tile (row*ld + slot), fixed
+    // per-lane byte offsets of this thread's DMA slots inside a tile (row*ldb + slot), fixed
     uint32_t doff[DMA_PER_WAVE];
 #pragma unroll
     for (int i = 0; i < DMA_PER_WAVE; i++) {
         const int P = (wave + 4 * i) * 64 + lane;
         const int row = P / SLOTS, sl = P % SLOTS;
-        doff[i] = (uint32_t)(row * a.ld_t + 4 * (sl == SLOTS - 1 ? 0 : sl)) * 4u;
+        doff[i] = (uint32_t)(row * ldb + 16 * (sl == SLOTS - 1 ? 0 : sl));
     }
     auto dma_tile = [&](int buf, int slot, int64_t r0) {
         typedef __attribute__((address_space(3))) void lds_void;
         typedef __attribute__((address_space(1))) const void gbl_void;
-        unsigned char* tile = reinterpret_cast<unsigned char*>(tiles + buf * TILE);
+        unsigned char* tile = tiles + buf * TILE;
         const bool tail = r0 + GF_BN > a.nt;  // block-uniform
-        const char* base = reinterpret_cast<const char*>(a.train + r0 * a.ld_t);
+        const unsigned char* base = trainb + r0 * ldb;
 #pragma unroll
         for (int i = 0; i < DMA_PER_WAVE; i++) {
             const int ins = wave + 4 * i;
             if (ins < DMA_INS) {
-                const char* src = base + doff[i];
+                const unsigned char* src = base + doff[i];
                 if (tail) {  // rows past nt re-read row nt-1 (their ring entries are +inf)
                     const int P = ins * 64 + lane;
                     const int row = P / SLOTS, sl = P % SLOTS;
                     const int64_t t = min(r0 + row, a.nt - 1);
-                    src = reinterpret_cast<const char*>(a.train + t * a.ld_t + 4 * (sl == SLOTS - 1 ? 0 : sl));
+                    src = trainb + t * ldb + 16 * (sl == SLOTS - 1 ? 0 : sl);
                 }
                 __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(tile + ins * 1024), 16, 0, 0);
             }
@@ -419,26 +462,32 @@ __global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
 
     // MFMAs of one tile into X, interleaved with the fast test of the previous tile (Y)
     auto step = [&](floatx16 (&X)[2], floatx16 (&Y)[2], int buf, int slotY) -> bool {
-        const float* tile = tiles + buf * TILE;
-        const float* a0p = tile + j * STRIDE + 4 * h;
-        const float* a1p = tile + (32 + j) * STRIDE + 4 * h;
+        const unsigned char* tile = tiles + buf * TILE;
+        const unsigned char* a0p = tile + j * STRIDE + 16 * h;
+        const unsigned char* a1p = tile + (32 + j) * STRIDE + 16 * h;
         const float* tnpY = ring + slotY * 2 * GF_BN;
         X[0] = floatx16{};
         X[1] = floatx16{};
         bool any = false;
         float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int g = 0; g < NG; g++) {
-            const float4 x0 = *reinterpret_cast<const float4*>(a0p + 8 * g);
-            const float4 x1 = *reinterpret_cast<const float4*>(a1p + 8 * g);
+        for (int s = 0; s < NS; s++) {
+            const uint4 x0 = *reinterpret_cast<const uint4*>(a0p + 32 * s);
+            const uint4 x1 = *reinterpret_cast<const uint4*>(a1p + 32 * s);
+            if constexpr (BF) {
+                const bf16x8 b = __builtin_bit_cast(bf16x8, qf[s]);
+                X[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, x0), b, X[0], 0, 0, 0);
+                X[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, x1), b, X[1], 0, 0, 0);
+            } else {
 #pragma unroll
-            for (int jj = 0; jj < 4; jj++) {
-                X[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(x0, jj), qf[4 * g + jj], X[0], 0, 0, 0);
-                X[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(x1, jj), qf[4 * g + jj], X[1], 0, 0, 0);
+                for (int jj = 0; jj < 4; jj++) {
+                    X[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(u4getf(x0, jj), u4getf(qf[s], jj), X[0], 0, 0, 0);
+                    X[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(u4getf(x1, jj), u4getf(qf[s], jj), X[1], 0, 0, 0);
+                }
             }
 #pragma unroll
             for (int vv = 0; vv < VPG; vv++) {
-                const int v = g * VPG + vv, rb = v >> 4, reg = v & 15;
+                const int v = s * VPG + vv, rb = v >> 4, reg = v & 15;
                 if ((reg & 3) == 0)
                     t4 = *reinterpret_cast<const float4*>(tnpY + 32 * rb + 8 * (reg >> 2) + 4 * h);
 #ifndef KNN_ABLATE_NO_EPI
@@ -568,13 +617,13 @@ __global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
-// k_rescore<R, CAPW>: one wave per query.  Final threshold = k-th smallest U among the
-// query's candidates (found by bisection over ordered float bits); candidates with
+// k_rescore<R, CAPW, E>: one wave per query.  Final threshold = k-th smallest U among
+// the query's candidates (found by bisection over ordered float bits); candidates with
 // L <= threshold are rescored with the exact direct form and selected by key.
 // Queries whose list overflowed (or holds < k entries) go to the exact fallback list.
 // LDS per wave: q row [ld_pad] f32 | counts [C] i32 | survivors [64*CAPW] i32
 // ---------------------------------------------------------------------------------
-template <int R, int CAPW>
+template <int R, int CAPW, typename E>
 __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
@@ -586,6 +635,8 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
     const int64_t q = (int64_t)blockIdx.x * 4 + wave;
     if (q >= a.nq) return;
     const int k = a.k;
+    const E* train = reinterpret_cast<const E*>(a.train);
+    const E* test = reinterpret_cast<const E*>(a.test);
     int total = 0;
     bool overflow = false;
     for (int sg = 0; sg < a.nseg; sg++) {
@@ -631,7 +682,7 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
         }
         m += __popcll(bal);
     }
-    for (int i = lane; i < a.d; i += 64) qs[i] = a.test[q * a.ld_q + i];
+    for (int i = lane; i < a.d; i += 64) qs[i] = widen(test[q * a.ld_q + i]);
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
 
@@ -643,7 +694,7 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
         u64 key = KEY_NONE;
         if (b + lane < m) {
             int32_t t = surv[b + lane];
-            key = make_key(direct_dist(qs, a.train + (int64_t)t * a.ld_t, a.d), (uint32_t)t);
+            key = make_key(direct_dist(qs, train + (int64_t)t * a.ld_t, a.d), (uint32_t)t);
         }
         bool pass = key < kth;
         if (__ballot(pass)) {
@@ -651,7 +702,88 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
             kth = list_at(T, k - 1);
         }
     }
-    finish_query<R>(T, k, a.C, a.labels, counts, q, a.pred, a.topk_dist, a.topk_idx, a.status);
+    finish_query<R>(T, k, a.C, a.labels, counts, q, a.out, a.status);
+}
+
+// ---------------------------------------------------------------------------------
+// k_merge_vote<R>: train-sharded runs.  Each of nsrc train shards gives
+// every query its exact k nearest rows as (dist bits, global idx, label), ascending.
+// One wave per query merges the nsrc*k keys with the same wave list, so ties keep the
+// lower GLOBAL index exactly like the reference's serial scan over the whole train set,
+// then votes over the k winners: a shard's winners are a prefix of its list, found by
+// key <= the k-th key.  LDS per wave: counts [C] i32.
+// ---------------------------------------------------------------------------------
+template <int R>
+__global__ __launch_bounds__(256) void k_merge_vote(MergeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = lane_id();
+    const int wave = threadIdx.x >> 6;
+    int* counts = reinterpret_cast<int*>(smem) + wave * ((a.C + 3) & ~3);
+    const int64_t q = (int64_t)blockIdx.x * 4 + wave;
+    if (q >= a.nq) return;
+    const int k = a.k;
+    u64 T[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) T[r] = KEY_NONE;
+    u64 kth = KEY_NONE;
+    for (int s = 0; s < a.nsrc; s++) {
+        const int32_t* rec = a.rec + ((int64_t)s * a.nq + q) * 3 * k;
+        for (int e0 = 0; e0 < k; e0 += 64) {
+            const int e = e0 + lane;
+            u64 key = KEY_NONE;
+            if (e < k) {
+                const int32_t ix = rec[k + e];
+                if (ix >= 0) key = make_key(__int_as_float(rec[e]), (uint32_t)ix);
+            }
+            const bool pass = key < kth;
+            if (__ballot(pass)) {
+                topk_merge<R>(T, pass ? key : KEY_NONE);
+                kth = list_at(T, k - 1);
+            }
+        }
+    }
+    const bool bad = (kth == KEY_NONE);
+    const QueryOut& o = a.out;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int e = 64 * r + lane;
+        if (e < k) {
+            const int64_t off = q * o.stride + e;
+            const u64 key = T[r];
+            if (o.dist) o.dist[off] = key == KEY_NONE ? FLT_MAX : __uint_as_float((uint32_t)(key >> 32));
+            if (o.idx) o.idx[off] = key == KEY_NONE ? -1 : (int32_t)(uint32_t)(key & 0xffffffffull);
+        }
+    }
+    if (!o.pred) return;
+    for (int c = lane; c < a.C; c += 64) counts[c] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int s = 0; s < a.nsrc; s++) {
+        const int32_t* rec = a.rec + ((int64_t)s * a.nq + q) * 3 * k;
+        for (int e = lane; e < k; e += 64) {
+            const int32_t ix = rec[k + e];
+            if (ix < 0) continue;
+            const u64 key = make_key(__int_as_float(rec[e]), (uint32_t)ix);
+            if (key <= kth && key != KEY_NONE) {
+                const int lab = rec[2 * k + e];
+                if (lab >= 0 && lab < a.C) atomicAdd(&counts[lab], 1);
+                else atomicOr(a.status, KNN_STATUS_BAD_LABEL);
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    u64 best = 0;
+    for (int c = lane; c < a.C; c += 64) {
+        u64 v = ((u64)(uint32_t)counts[c] << 32) | (u64)(0xffffffffu - (uint32_t)c);
+        best = umax64(best, v);
+    }
+#pragma unroll
+    for (int j = 32; j > 0; j >>= 1) best = umax64(best, __shfl_xor(best, j));
+    if (lane == 0) {
+        o.pred[q] = bad ? 0 : (int32_t)(0xffffffffu - (uint32_t)(best & 0xffffffffull));
+        if (bad) atomicOr(a.status, KNN_STATUS_TOO_FEW);
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -698,68 +830,105 @@ __global__ __launch_bounds__(256) void k_generate(GenerateArgs a) {
 
 static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-template <int R>
+// k <= 64R selects the wave-list register count R
+static int list_regs(int k) { return k <= 64 ? 1 : k <= 128 ? 2 : k <= 256 ? 4 : k <= 512 ? 8 : 16; }
+
+template <int R, typename E>
 static hipError_t launch_exact_r(const ExactScanArgs& a0, int grid, hipStream_t st) {
     ExactScanArgs a = a0;
     a.q_lds_bytes = (int)align16((size_t)a.d * sizeof(float));
     size_t lds = a.q_lds_bytes + 4 * 64 * R * sizeof(u64) + align16((size_t)a.C * sizeof(int));
-    hipLaunchKernelGGL(k_exact_scan<R>, dim3(grid), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((k_exact_scan<R, E>), dim3(grid), dim3(256), lds, st, a);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
+}
+
+template <typename E>
+static hipError_t launch_exact_e(const ExactScanArgs& a, int grid, hipStream_t st) {
+    switch (list_regs(a.k)) {
+        case 1: return launch_exact_r<1, E>(a, grid, st);
+        case 2: return launch_exact_r<2, E>(a, grid, st);
+        case 4: return launch_exact_r<4, E>(a, grid, st);
+        case 8: return launch_exact_r<8, E>(a, grid, st);
+        default: return launch_exact_r<16, E>(a, grid, st);
+    }
 }
 
 hipError_t knn_launch_exact_scan(const ExactScanArgs& a, int grid, hipStream_t st) {
-    if (a.k <= 64) return launch_exact_r<1>(a, grid, st);
-    if (a.k <= 128) return launch_exact_r<2>(a, grid, st);
-    if (a.k <= 256) return launch_exact_r<4>(a, grid, st);
-    if (a.k <= 512) return launch_exact_r<8>(a, grid, st);
-    return launch_exact_r<16>(a, grid, st);
+    return a.elem == ELEM_BF16 ? launch_exact_e<bf16_t>(a, grid, st) : launch_exact_e<float>(a, grid, st);
 }
 
 size_t knn_exact_scan_lds(int d, int k, int C) {
-    int R = k <= 64 ? 1 : k <= 128 ? 2 : k <= 256 ? 4 : k <= 512 ? 8 : 16;
-    return align16((size_t)d * 4) + 4 * 64 * (size_t)R * 8 + align16((size_t)C * 4);
+    return align16((size_t)d * 4) + 4 * 64 * (size_t)list_regs(k) * 8 + align16((size_t)C * 4);
 }
 
-hipError_t knn_launch_row_norms(const float* x, int64_t n, int ld, int d, float* out,
+hipError_t knn_launch_row_norms(const void* x, int elem, int64_t n, int ld, int d, float* out,
                                 int32_t* status, uint32_t* maxo, float* outp, float c1, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const int64_t rows = n + (outp ? 64 : 0);
-    hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, x, n, ld, d,
-                       out, status, maxo, outp, c1);
+    dim3 grid((unsigned)((rows + 255) / 256));
+    if (elem == ELEM_BF16)
+        hipLaunchKernelGGL(k_row_norms<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, n, ld, d, out,
+                           status, maxo, outp, c1);
+    else
+        hipLaunchKernelGGL(k_row_norms<float>, grid, dim3(256), 0, st, (const float*)x, n, ld, d, out,
+                           status, maxo, outp, c1);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }
 
-size_t knn_gemm_filter_lds(int dk, int k) {
-    return (2 * (size_t)GF_BN * (dk + 4) + 3 * 2 * GF_BN + (size_t)GF_BM * k) * sizeof(float) +
+size_t knn_gemm_filter_lds(int row_bytes, int k) {
+    return 2 * (size_t)GF_BN * (row_bytes + 16) + (3 * 2 * GF_BN + (size_t)GF_BM * k) * sizeof(float) +
            GF_BM * sizeof(int);
 }
 
-template <int DK>
-static const void* gemm_filter_fn() { return reinterpret_cast<const void*>(&k_gemm_filter<DK>); }
-
-hipError_t knn_gemm_filter_occupancy(int dk, int k, int* blocks_per_cu) {
-    size_t lds = knn_gemm_filter_lds(dk, k);
-    const void* fn = dk == 32 ? gemm_filter_fn<32>()
-                   : dk == 64 ? gemm_filter_fn<64>() : gemm_filter_fn<128>();
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 256, lds);
+bool knn_gemm_filter_supported(int elem, int row_bytes) {
+    (void)elem;
+    return row_bytes == 128 || row_bytes == 256 || row_bytes == 512;
 }
 
-hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int dk, hipStream_t st) {
-    size_t lds = knn_gemm_filter_lds(dk, a.k);
-    dim3 grid((unsigned)(a.n_qtiles * a.nseg));
-    switch (dk) {
-        case 32: hipLaunchKernelGGL(k_gemm_filter<32>, grid, dim3(256), lds, st, a); break;
-        case 64: hipLaunchKernelGGL(k_gemm_filter<64>, grid, dim3(256), lds, st, a); break;
-        case 128: hipLaunchKernelGGL(k_gemm_filter<128>, grid, dim3(256), lds, st, a); break;
-        default: return hipErrorInvalidValue;
-    }
+template <typename E, int RB>
+static const void* gemm_filter_fn() { return reinterpret_cast<const void*>(&k_gemm_filter<E, RB>); }
+
+static const void* gemm_filter_ptr(int elem, int row_bytes) {
+    if (elem == ELEM_BF16)
+        return row_bytes == 128 ? gemm_filter_fn<bf16_t, 128>()
+             : row_bytes == 256 ? gemm_filter_fn<bf16_t, 256>() : gemm_filter_fn<bf16_t, 512>();
+    return row_bytes == 128 ? gemm_filter_fn<float, 128>()
+         : row_bytes == 256 ? gemm_filter_fn<float, 256>() : gemm_filter_fn<float, 512>();
+}
+
+hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks_per_cu) {
+    if (!knn_gemm_filter_supported(elem, row_bytes)) return hipErrorInvalidValue;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, gemm_filter_ptr(elem, row_bytes), 256,
+                                                        knn_gemm_filter_lds(row_bytes, k));
+}
+
+template <typename E, int RB>
+static hipError_t launch_gemm_filter_t(const GemmFilterArgs& a, hipStream_t st) {
+    const size_t lds = knn_gemm_filter_lds(RB, a.k);
+    hipLaunchKernelGGL((k_gemm_filter<E, RB>), dim3((unsigned)(a.n_qtiles * a.nseg)), dim3(256), lds, st, a);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }
 
-template <int R>
+hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st) {
+    if (!knn_gemm_filter_supported(elem, row_bytes)) return hipErrorInvalidValue;
+    if (elem == ELEM_BF16) {
+        switch (row_bytes) {
+            case 128: return launch_gemm_filter_t<bf16_t, 128>(a, st);
+            case 256: return launch_gemm_filter_t<bf16_t, 256>(a, st);
+            default: return launch_gemm_filter_t<bf16_t, 512>(a, st);
+        }
+    }
+    switch (row_bytes) {
+        case 128: return launch_gemm_filter_t<float, 128>(a, st);
+        case 256: return launch_gemm_filter_t<float, 256>(a, st);
+        default: return launch_gemm_filter_t<float, 512>(a, st);
+    }
+}
+
+template <int R, typename E>
 static hipError_t launch_rescore_r(const RescoreArgs& a0, hipStream_t st) {
     RescoreArgs a = a0;
     a.q_lds_bytes = (int)align16((size_t)a.d * 4);
@@ -768,17 +937,44 @@ static hipError_t launch_rescore_r(const RescoreArgs& a0, hipStream_t st) {
     size_t lds = 4 * (size_t)a.wave_lds_bytes;
     unsigned grid = (unsigned)((a.nq + 3) / 4);
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((k_rescore<R, KNN_RESCORE_CAPW>), dim3(grid), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((k_rescore<R, KNN_RESCORE_CAPW, E>), dim3(grid), dim3(256), lds, st, a);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }
 
+template <typename E>
+static hipError_t launch_rescore_e(const RescoreArgs& a, hipStream_t st) {
+    switch (list_regs(a.k)) {
+        case 1: return launch_rescore_r<1, E>(a, st);
+        case 2: return launch_rescore_r<2, E>(a, st);
+        case 4: return launch_rescore_r<4, E>(a, st);
+        case 8: return launch_rescore_r<8, E>(a, st);
+        default: return launch_rescore_r<16, E>(a, st);
+    }
+}
+
 hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st) {
-    if (a.k <= 64) return launch_rescore_r<1>(a, st);
-    if (a.k <= 128) return launch_rescore_r<2>(a, st);
-    if (a.k <= 256) return launch_rescore_r<4>(a, st);
-    if (a.k <= 512) return launch_rescore_r<8>(a, st);
-    return launch_rescore_r<16>(a, st);
+    return a.elem == ELEM_BF16 ? launch_rescore_e<bf16_t>(a, st) : launch_rescore_e<float>(a, st);
+}
+
+template <int R>
+static hipError_t launch_merge_r(const MergeArgs& a, hipStream_t st) {
+    const unsigned grid = (unsigned)((a.nq + 3) / 4);
+    if (grid == 0) return hipSuccess;
+    const size_t lds = 4 * (size_t)((a.C + 3) & ~3) * sizeof(int);
+    hipLaunchKernelGGL(k_merge_vote<R>, dim3(grid), dim3(256), lds, st, a);
+    KNN_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t knn_launch_merge(const MergeArgs& a, hipStream_t st) {
+    switch (list_regs(a.k)) {
+        case 1: return launch_merge_r<1>(a, st);
+        case 2: return launch_merge_r<2>(a, st);
+        case 4: return launch_merge_r<4>(a, st);
+        case 8: return launch_merge_r<8>(a, st);
+        default: return launch_merge_r<16>(a, st);
+    }
 }
 
 hipError_t knn_launch_generate(const GenerateArgs& a, hipStream_t st) {

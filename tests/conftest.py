@@ -138,3 +138,28 @@ def golden_cm(ds, k):
 
 def pred_sha(pred):
     return hashlib.sha256("".join(f"{int(p)}\n" for p in pred).encode()).hexdigest()
+
+
+def merge_lists_reference(rec, k, C):
+    """Host restatement of k_merge_vote (test infrastructure): rec [nsrc][nq][3][k] int32
+    per-shard lists (dist bits, global idx or -1, label) -> (pred, dist, idx) of the k
+    smallest (dist, idx) over all shards, vote = bincount argmax (smallest label on ties,
+    main.cpp:64-78)."""
+    rec = np.asarray(rec)
+    nsrc, nq = rec.shape[0], rec.shape[1]
+    pred = np.zeros(nq, np.int32)
+    dist = np.full((nq, k), np.finfo(np.float32).max, np.float32)
+    idx = np.full((nq, k), -1, np.int32)
+    for q in range(nq):
+        r = rec[:, q]                                   # [nsrc][3][k]
+        d = r[:, 0, :].reshape(-1).view(np.uint32)
+        i = r[:, 1, :].reshape(-1)
+        lab = r[:, 2, :].reshape(-1)
+        ok = i >= 0
+        d, i, lab = d[ok], i[ok], lab[ok]
+        order = np.lexsort((i, d))[:k]
+        n = len(order)
+        dist[q, :n] = d[order].view(np.float32)
+        idx[q, :n] = i[order]
+        pred[q] = int(np.argmax(np.bincount(lab[order], minlength=C))) if n == k else 0
+    return pred, dist, idx

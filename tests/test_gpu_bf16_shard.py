@@ -1,0 +1,174 @@
+"""GPU parity for bf16 features and the train-sharded path.
+
+bf16 features are checked against the oracle run on the exactly widened fp32 values
+(what the reference computes on those numbers); train-sharded runs (per-shard exact
+top-k -> merge + vote) against the oracle's serial KNN over the whole train set.
+Bar: bit-exact predictions, neighbour indices and distance bits.
+"""
+import numpy as np
+import pytest
+
+from conftest import merge_lists_reference
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctxs(knn):
+    out = {a: knn.Context(0, algo=a) for a in ("direct", "gemm", "auto")}
+    yield out
+    for c in out.values():
+        c.close()
+
+
+def _bf16_grid(oracle, knn, seed, stream, n, d):
+    """bf16-exact synthetic rows (generator kind 1)."""
+    f, lab = oracle.gen(seed, stream, 0, n, d, kind=1)
+    return knn.to_bf16_bits(f), f, lab
+
+
+def _bf16_random(knn, rng, n, d, scale=1.0):
+    """bf16 rows that are NOT on a coarse grid: distances round in fp32."""
+    bits = knn.to_bf16_bits(rng.standard_normal((n, d)).astype(np.float32) * scale)
+    return bits, knn.bf16_bits_to_f32(bits)
+
+
+def test_bf16_conversions(knn):
+    x = np.array([1.0, -2.5, 0.0, 3.140625, 2.0**-130, -0.0], np.float32)
+    assert np.array_equal(knn.bf16_bits_to_f32(knn.to_bf16_bits(x)).view(np.uint32), x.view(np.uint32))
+
+
+@pytest.mark.parametrize("d,k,nt,nq", [(256, 100, 20000, 130), (256, 10, 9000, 300), (128, 32, 12000, 129),
+                                       (64, 1, 5000, 70), (256, 128, 8192, 64), (200, 7, 3000, 40)])
+def test_bf16_grid_vs_oracle(knn, oracle, ctxs, d, k, nt, nq):
+    trb, trf, tl = _bf16_grid(oracle, knn, 3, 0, nt, d)
+    teb, tef, _ = _bf16_grid(oracle, knn, 3, 1, nq, d)
+    bad, opred, odist, oidx = oracle.knn(trf, tl, tef, k, 10)
+    assert bad == 0
+    for algo in ("direct", "gemm"):
+        pred, dist, idx = ctxs[algo].predict(trb, tl, teb, k, 10, topk=True)
+        if algo == "gemm" and d in (64, 128, 256):
+            assert ctxs[algo].stats()["train_segments"] >= 1, "bf16 MFMA filter did not run"
+        assert np.array_equal(idx, oidx), algo
+        assert np.array_equal(dist.view(np.uint32), odist.view(np.uint32)), algo
+        assert np.array_equal(pred, opred), algo
+
+
+@pytest.mark.parametrize("d,k,scale", [(256, 100, 1.0), (128, 16, 1e-3), (64, 5, 3e4)])
+def test_bf16_random_vs_oracle(knn, oracle, ctxs, d, k, scale):
+    rng = np.random.default_rng(d + k)
+    trb, trf = _bf16_random(knn, rng, 15000, d, scale)
+    teb, tef = _bf16_random(knn, rng, 150, d, scale)
+    tl = rng.integers(0, 10, size=15000).astype(np.int32)
+    bad, opred, odist, oidx = oracle.knn(trf, tl, tef, k, 10)
+    pred, dist, idx = ctxs["gemm"].predict(trb, tl, teb, k, 10, topk=True)
+    assert ctxs["gemm"].stats()["train_segments"] >= 1
+    assert np.array_equal(idx, oidx)
+    assert np.array_equal(dist.view(np.uint32), odist.view(np.uint32))
+    assert np.array_equal(pred, opred)
+
+
+def test_bf16_generator_matches_oracle(knn, oracle):
+    import torch
+    c = knn.Context(0)
+    feat = torch.empty((555, 256), dtype=torch.bfloat16, device="cuda:0")
+    lab = torch.empty(555, dtype=torch.int32, device="cuda:0")
+    c.generate(feat, lab, 77, 256, 1, 3, 0, 10)
+    of, ol = oracle.gen(3, 0, 77, 555, 256, kind=1)
+    assert np.array_equal(feat.view(torch.int16).cpu().numpy().view(np.uint16), knn.to_bf16_bits(of))
+    assert np.array_equal(lab.cpu().numpy(), ol)
+    c.close()
+
+
+def _shard_run(knn, ctx, train, labels, test, k, C, bounds):
+    """Per-shard top-k on one GPU for each [a, b) in bounds, then merge + vote."""
+    import torch
+    recs = []
+    for a, b in bounds:
+        rec = torch.empty((test.shape[0], 3, k), dtype=torch.int32, device="cuda:0")
+        ctx.shard_topk_device(train[a:b], labels[a:b], test, k, C, a, rec)
+        recs.append(rec)
+    allrec = torch.stack(recs)
+    pred = torch.empty(test.shape[0], dtype=torch.int32, device="cuda:0")
+    dist = torch.empty((test.shape[0], k), dtype=torch.float32, device="cuda:0")
+    idx = torch.empty((test.shape[0], k), dtype=torch.int32, device="cuda:0")
+    ctx.merge_vote_device(allrec, k, C, pred, dist, idx)
+    return allrec.cpu().numpy(), pred.cpu().numpy(), dist.cpu().numpy(), idx.cpu().numpy()
+
+
+@pytest.mark.parametrize("dtype,d,k,nt,nq,bounds", [
+    ("bf16", 256, 100, 24000, 100, [(0, 8000), (8000, 16000), (16000, 24000)]),
+    ("f32", 128, 10, 20000, 257, [(0, 5000), (5000, 17000), (17000, 20000)]),
+    ("f32", 64, 32, 9000, 64, [(0, 4500), (4500, 9000)]),
+    ("bf16", 128, 40, 5000, 33, [(0, 30), (30, 4000), (4000, 5000)]),   # k > a shard's rows
+])
+@pytest.mark.parametrize("algo", ["direct", "gemm"])
+def test_train_sharded_matches_serial(knn, oracle, ctxs, dtype, d, k, nt, nq, bounds, algo):
+    import torch
+    kind = 1 if dtype == "bf16" else 0
+    trf, tl = oracle.gen(11, 0, 0, nt, d, kind=kind)
+    tef, _ = oracle.gen(11, 1, 0, nq, d, kind=kind)
+    bad, opred, odist, oidx = oracle.knn(trf, tl, tef, k, 10)
+    assert bad == 0
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    train = torch.from_numpy(trf).to("cuda:0").to(tdt)
+    test = torch.from_numpy(tef).to("cuda:0").to(tdt)
+    labels = torch.from_numpy(tl).to("cuda:0")
+    allrec, pred, dist, idx = _shard_run(knn, ctxs[algo], train, labels, test, k, 10, bounds)
+    assert np.array_equal(idx, oidx)
+    assert np.array_equal(dist.view(np.uint32), odist.view(np.uint32))
+    assert np.array_equal(pred, opred)
+    # the host restatement of the merge (used by the gloo tests) agrees with the kernel
+    mp, md, mi = merge_lists_reference(allrec, k, 10)
+    assert np.array_equal(mp, pred) and np.array_equal(mi, idx)
+
+
+def test_train_sharded_errors(knn, ctxs):
+    import torch
+    c = ctxs["auto"]
+    test = torch.zeros((4, 64), dtype=torch.float32, device="cuda:0")
+    train = torch.zeros((2, 64), dtype=torch.float32, device="cuda:0")
+    labels = torch.zeros(2, dtype=torch.int32, device="cuda:0")
+    rec = torch.empty((4, 3, 3), dtype=torch.int32, device="cuda:0")
+    c.shard_topk_device(train, labels, test, 3, 2, 0, rec)        # k > shard rows: fine
+    r = rec.cpu().numpy()
+    assert (r[:, 1, 2] == -1).all() and (r[:, 1, :2] >= 0).all()
+    pred = torch.empty(4, dtype=torch.int32, device="cuda:0")
+    with pytest.raises(knn.KnnError) as e:                        # 2 neighbours in total < k
+        c.merge_vote_device(rec[None], 3, 2, pred)
+    assert e.value.status == knn.KNN_ERANGE
+    with pytest.raises(knn.KnnError) as e:                        # global index overflow
+        c.shard_topk_device(train, labels, test, 3, 2, 2**31 - 2, rec)
+    assert e.value.status == knn.KNN_EINVAL
+
+
+def test_config_c_shard_sampled(knn, oracle):
+    """A config C rank's shard at reduced query count: 1M bf16 train rows x 20k queries x
+    256-d, k = 100, through the bf16 MFMA filter; 24 sampled queries checked bit-exactly
+    against the oracle over the shard, plus size-independent properties."""
+    import torch
+    nt, nq, d, k = 1_000_000, 20_000, 256, 100
+    c = knn.Context(0, algo="auto", profile=True)
+    train = torch.empty((nt, d), dtype=torch.bfloat16, device="cuda:0")
+    labels = torch.empty(nt, dtype=torch.int32, device="cuda:0")
+    test = torch.empty((nq, d), dtype=torch.bfloat16, device="cuda:0")
+    c.generate(train, labels, 0, d, 1, 3, 0, 10)
+    c.generate(test, None, 0, d, 1, 3, 1, 10)
+    rec = torch.empty((nq, 3, k), dtype=torch.int32, device="cuda:0")
+    base = 3_000_000
+    c.shard_topk_device(train, labels, test, k, 10, base, rec)
+    assert c.stats()["train_segments"] >= 1
+    r = rec.cpu().numpy()
+    dd = r[:, 0, :].view(np.float32)
+    ii = r[:, 1, :]
+    assert np.all(np.diff(dd.view(np.uint32).astype(np.int64), axis=1) >= 0)
+    assert ii.min() >= base and ii.max() < base + nt
+    qs = np.linspace(0, nq - 1, 24).astype(np.int64)
+    trf = train.float().cpu().numpy()
+    tef = test.float().cpu().numpy()[qs]
+    lab = labels.cpu().numpy()
+    bad, _, odist, oidx = oracle.knn(trf, lab, tef, k, 10)
+    assert np.array_equal(ii[qs] - base, oidx)
+    assert np.array_equal(dd[qs].view(np.uint32), odist.view(np.uint32))
+    assert np.array_equal(r[qs, 2, :], lab[oidx])
+    c.close()
