@@ -93,6 +93,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--algo", default="auto", choices=["auto", "gemm", "direct"])
     ap.add_argument("--splits", type=int, default=0, help="train segments per query tile (0 = auto)")
+    ap.add_argument("--nt", type=int, default=0, help="override train rows (kernel studies)")
+    ap.add_argument("--nq", type=int, default=0, help="override query rows (kernel studies)")
     args = ap.parse_args()
 
     import torch
@@ -119,6 +121,7 @@ def main():
     spec.loader.exec_module(knn)
 
     nt, nq_cfg, d, k, C, seed, scaling, dtype, sharding = CONFIGS[args.config]
+    nt, nq_cfg = args.nt or nt, args.nq or nq_cfg
     kind = 1 if dtype == "bf16" else 0                  # bf16-exact generator values for bf16
     tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
     dev = torch.device("cuda", local)

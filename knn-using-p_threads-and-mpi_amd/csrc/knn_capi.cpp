@@ -130,7 +130,7 @@ int choose_algo(const knn_ctx* c, int64_t nt, int64_t nq, int d, int k, int dtyp
     // (128, 256 or 512 bytes: fp32 d = 32/64/128, bf16 d = 64/128/256)
     const int rb = d * elem_size(dtype);
     bool gemm_ok = knn_gemm_filter_supported(dtype, rb) && k <= 128 && k <= nt &&
-                   knn_gemm_filter_lds(rb, k) <= 160 * 1024;
+                   knn_gemm_filter_lds(dtype, rb, k) <= 160 * 1024;
     if (c->algo == KNN_ALGO_GEMM) return gemm_ok ? KNN_ALGO_GEMM : KNN_ALGO_DIRECT;
     // AUTO: the direct form wins at low d (3 VALU ops per dim, no rescore) and on small jobs
     if (gemm_ok && d >= 32 && nt >= 8192 && (double)nt * (double)nq >= 1e9) return KNN_ALGO_GEMM;
@@ -252,7 +252,8 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     HIP_OR_FAIL(c, hipMemsetD32Async((hipDeviceptr_t)c->gthr.p, 0xFF800000u, nq, st));  // ordered(+inf)
     stage_end(c, st);
 
-    const int64_t n_qtiles = (nq + 127) / 128;
+    const FilterPlan plan = knn_gemm_filter_plan(dtype, rb, k);
+    const int64_t n_qtiles = (nq + plan.bm - 1) / plan.bm;
     const int nseg = choose_splits(c, n_qtiles, nt, dtype, rb, k, cap);
     int64_t seg_len = (nt + nseg - 1) / nseg;
     seg_len = (seg_len + 63) / 64 * 64;

@@ -72,8 +72,13 @@ hipError_t knn_launch_row_norms(const void* x, int elem, int64_t n, int ld, int 
                                 int32_t* status, uint32_t* maxo, float* outp, float c1, hipStream_t st);
 // row_bytes = d * element size: 128, 256 or 512
 bool knn_gemm_filter_supported(int elem, int row_bytes);
+// block shape of the filter for (element type, row bytes, k): waves per block, query
+// groups per wave, row groups per tile, min waves per SIMD (launch bounds), tile buffers,
+// queries per block, LDS bytes per block
+struct FilterPlan { int nw, qg, rg, minw, nbuf, bm; size_t lds; };
+FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k);
 hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st);
-size_t knn_gemm_filter_lds(int row_bytes, int k);
+size_t knn_gemm_filter_lds(int elem, int row_bytes, int k);
 hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks_per_cu);
 hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st);
 hipError_t knn_launch_merge(const MergeArgs& a, hipStream_t st);

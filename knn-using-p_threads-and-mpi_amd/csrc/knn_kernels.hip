@@ -27,6 +27,9 @@
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdint.h>
+#include <stdlib.h>
+
+#include <string>
 
 #include "knn_kernels.h"
 
@@ -232,6 +235,9 @@ __global__ __launch_bounds__(256) void k_exact_scan(ExactScanArgs a) {
     int* counts = reinterpret_cast<int*>(smem + a.q_lds_bytes + 4 * 64 * R * sizeof(u64));
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
+#if defined(KNN_ABLATE_NO_SLOW) || defined(KNN_ABLATE_NO_EPI) || defined(KNN_ABLATE_NO_DMA)
+    if (a.qlist) return;  // ablation builds time the filter only: skip the fallback scan
+#endif
     const int64_t n_work = a.qlist ? (int64_t)(*a.qcount) : a.nq;
     const E* train = reinterpret_cast<const E*>(a.train);
     const E* test = reinterpret_cast<const E*>(a.test);
@@ -326,37 +332,42 @@ __global__ __launch_bounds__(256) void k_row_norms(const E* __restrict__ x, int6
 }
 
 // ---------------------------------------------------------------------------------
-// k_gemm_filter<E, RB>: GEMM-form candidate filter on MFMA.  E = float (RB/4-d rows,
-// v_mfma_f32_32x32x2_f32, exact fp32) or bf16 (RB/2-d rows, v_mfma_f32_32x32x16_bf16);
-// RB = bytes per row (128, 256, 512).
+// k_gemm_filter<E, RB, MINB, NBUF, QG>: GEMM-form candidate filter on MFMA.
+//   E = float (RB/4-d rows, v_mfma_f32_32x32x2_f32, exact fp32) or bf16 (RB/2-d rows,
+//   v_mfma_f32_32x32x16_bf16); RB = bytes per row (128, 256, 512).
 //
-// Block = 256 threads = 4 waves.  Query tile BM = 128 (32 per wave): each lane keeps
-// 16 bytes of its query row per k-step s (bytes [32s+16h, 32s+16h+16), h = lane>>5) as
-// the B-operand fragment, in VGPRs for the whole scan.  Train tiles of BN = 64 rows are
-// copied global -> LDS by LDS-DMA (global_load_lds_dwordx4, no staging registers),
-// double-buffered with one barrier per tile (the barrier's vmcnt(0) retires the DMA
-// issued one tile earlier).  Rows keep natural k order and are padded to RB+16 bytes
-// (the pad slot of each row receives a harmless duplicate) so the A-operand
-// ds_read_b128 is conflict-free; lane (j,h) reads the same 16 bytes of train rows j and
-// 32+j as its query fragment: fp32 feeds 4 k-steps of 32x32x2 (k = 8s+4h+jj), bf16 one
+// Block = 256 threads = 4 waves; each wave owns QG groups of 32 queries (BM = 128 QG
+// per block); a train tile holds BN = 32 RG rows with RG = 2 / QG, so every wave runs
+// two 32x32 accumulators per tile either way: (rows 0-31, rows 32-63) x its 32 queries
+// for QG = 1 (fp32: MFMA-bound, fewer heaps), or rows 0-31 x (queries 0-31, 32-63) for
+// QG = 2 (bf16: a 32x32x16 MFMA moves 16x the FLOP of the fp32 one, so the train bytes
+// per FLOP must halve -- twice the queries per staged byte -- to stay under what L2 ->
+// LDS delivers per CU, and each A fragment read feeds two MFMAs).
+// Each lane keeps 16 bytes of its query rows per k-step s (bytes [32s+16h, 32s+16h+16),
+// h = lane>>5) as B-operand fragments, in VGPRs for the whole scan.  Train tiles are
+// copied global -> LDS by LDS-DMA (global_load_lds_dwordx4, no staging registers), NBUF
+// buffers deep with one barrier per tile.  Rows keep natural k order and are padded to
+// RB+16 bytes (the pad slot of each row receives a harmless duplicate) so the A-operand
+// ds_read_b128 is conflict-free; lane (j,h) reads the same 16 bytes of train row j (and
+// 32+j) as its query fragment: fp32 feeds 4 k-steps of 32x32x2 (k = 8s+4h+jj), bf16 one
 // 32x32x16 (k = 16s+8h+jj, the gfx950 A/B lane map).  Per tile each wave issues the
-// MFMAs of a 64 (train) x 32 (query) block into accumulator set X while the certified
-// test of the PREVIOUS tile (set Y) runs in between (software pipelining); lane l holds
-// query l&31 and train rows (reg&3)+8(reg>>2)+4(l>>5) (+32 for the second block).
+// tile's MFMAs into accumulator set X while the certified test of the PREVIOUS tile
+// (set Y) runs in between (software pipelining).  Accumulator a of a lane l holds
+// query group qg(a), train row 32 rg(a) + (reg&3) + 8(reg>>2) + 4(l>>5), column l&31.
 //
 // Certificate: with s = qn+tn, G = fma(-2, q.t, s), Delta = coef*s+eta,
 // L = G - Delta <= D <= U = G + Delta for the reference's direct-form distance D
 // (coef/eta per element type, set by the host).
 // A row is kept for query q iff L <= thr_q, thr_q = the k-th smallest U among rows
-// this block kept (sorted list in LDS) or a smaller bound published by another
-// segment (gthr).  Every row of the exact top-k has L <= D <= D_(k) <= thr_q.
-// The per-value fast test y = fma(-2, q.t, (1-coef) tn) <= tf_q is a conservative
-// superset of L <= thr_q (tf_q adds 2^-16 (|thr|+qn+max tn) > the rounding gap of
-// the two formulas); a wave re-checks exactly only when some lane passes (slow path).
-// Kept rows go to this segment's slice of the query's candidate list (LDS counter).
+// this block kept (the root of a per-query max-heap of the k smallest U, in LDS) or a
+// smaller bound published by another segment (gthr).  Every row of the exact top-k
+// has L <= D <= D_(k) <= thr_q.  The per-value fast test y = fma(-2, q.t, (1-coef) tn)
+// <= tf_q is a conservative superset of L <= thr_q (tf_q adds 2^-16 (|thr|+qn+max tn)
+// > the rounding gap of the two formulas); a wave re-checks exactly only when some lane
+// passes (slow path).  Kept rows go to this segment's slice of the query's candidate
+// list (LDS counter).
 // ---------------------------------------------------------------------------------
-static constexpr int GF_BM = 128;
-static constexpr int GF_BN = 64;
+static constexpr int GF_BM1 = 128;  // queries per block per query group
 
 __device__ __forceinline__ float f4get(const float4& v, int i) {
     return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
@@ -365,22 +376,77 @@ __device__ __forceinline__ float u4getf(const uint4& v, int i) {
     return __uint_as_float(i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w);
 }
 
-template <typename E, int RB>
-__global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
+// LDS-DMA issued by inline asm: the compiler does not see these as LDS writes, so it
+// does not put a vmcnt(0) in front of the next LDS read (which would serialise every
+// tile's compute behind the DMA of the tile after it); the kernel orders them itself
+// with counted waits + s_barrier (wait_dma_barrier).  M0 = LDS destination (uniform).
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(lds)
+                 : "memory", "m0");
+}
+// scalar base + 32-bit per-lane offset (no per-lane 64-bit address math in the loop)
+__device__ __forceinline__ void dma16s(uint32_t voff, const void* sbase, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds)
+                 : "memory", "m0");
+}
+__device__ __forceinline__ void dma4s(uint32_t voff, const void* sbase, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sbase), "s"(lds)
+                 : "memory", "m0");
+}
+// wait until at most n (wave-uniform, <= 15) vector-memory ops of this wave are in
+// flight, then barrier: vmcnt retires in issue order for loads (the DMAs)
+__device__ __forceinline__ void wait_dma_barrier(int n) {
+#define KNN_WAIT_CASE(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")\n\ts_barrier" ::: "memory"); break;
+    switch (n) {
+        KNN_WAIT_CASE(1) KNN_WAIT_CASE(2) KNN_WAIT_CASE(3) KNN_WAIT_CASE(4) KNN_WAIT_CASE(5)
+        KNN_WAIT_CASE(6) KNN_WAIT_CASE(7) KNN_WAIT_CASE(8) KNN_WAIT_CASE(9) KNN_WAIT_CASE(10)
+        KNN_WAIT_CASE(11) KNN_WAIT_CASE(12) KNN_WAIT_CASE(13) KNN_WAIT_CASE(14) KNN_WAIT_CASE(15)
+        default: asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    }
+#undef KNN_WAIT_CASE
+}
+
+// per-query heap stride in floats: slot 0 unused, heap in [1, k], slots past k hold -inf
+// (so a sibling pair H[2i], H[2i+1] is one aligned 8-byte read)
+__host__ __device__ __forceinline__ int heap_stride(int k) { return (k + 2) & ~1; }
+
+// tile geometry shared by the kernel and the host's LDS sizing: NW waves per block,
+// QG 32-query groups per wave, RG 32-row groups per tile; NACC = QG * RG accumulators
+template <int RB, int NW, int QG, int RG>
+struct FilterTile {
+    static constexpr int NACC = QG * RG;             // 32x32 accumulators per wave per tile
+    static constexpr int BN = 32 * RG;               // train rows per tile
+    static constexpr int BM = 32 * QG * NW;          // queries per block
+    static constexpr int STRIDE = RB + 16;           // LDS bytes per tile row
+    static constexpr int SLOTS = RB / 16 + 1;        // 16-B slots per padded row
+    static constexpr int DMA_INS = (BN * SLOTS + 63) / 64;     // 1 KiB DMA instructions per tile
+    static constexpr int LAST_LANES = BN * SLOTS - 64 * (DMA_INS - 1);  // active lanes of the last
+    static constexpr int TILE = DMA_INS * 1024;      // LDS bytes per buffer (>= BN * STRIDE)
+};
+
+template <typename E, int RB, int MINW, int NBUF, int NW, int QG, int RG>
+__global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a) {
+    typedef FilterTile<RB, NW, QG, RG> FT;
     constexpr bool BF = sizeof(E) == 2;
-    constexpr int STRIDE = RB + 16;          // bytes per LDS tile row (pad: conflict-free b128)
-    constexpr int TILE = GF_BN * STRIDE;
-    constexpr int NS = RB / 32;              // k-steps: 16 B per lane half per step
-    constexpr int SLOTS = RB / 16 + 1;       // 16-B slots per padded LDS row
-    constexpr int DMA_INS = GF_BN * SLOTS / 64;          // 1 KiB LDS-DMA instructions per tile
-    constexpr int DMA_PER_WAVE = (DMA_INS + 3) / 4;
-    constexpr int VPG = 32 / NS;             // epilogue values interleaved per k-step
-    static_assert(GF_BN * SLOTS % 64 == 0 && 32 % NS == 0, "tile geometry");
+    constexpr int NACC = FT::NACC, BN = FT::BN, BM = FT::BM, STRIDE = FT::STRIDE, SLOTS = FT::SLOTS;
+    constexpr int DMA_INS = FT::DMA_INS, TILE = FT::TILE;
+    constexpr int NT = 64 * NW;                    // threads per block
+    constexpr int DMA_PER_WAVE = (DMA_INS + NW - 1) / NW;
+    constexpr int NS = RB / 32;                    // k-steps: 16 B per lane half per step
+    constexpr int NV = 16 * NACC;                  // fast-test values per lane per tile
+    constexpr int VPS = 16 / NS;                   // values per accumulator per k-step
+    constexpr int NR = NBUF + 1;                   // norm ring slots: tiles it-1 .. it+NBUF-1
+    static_assert(16 % NS == 0 && (NACC == 1 || NACC == 2) && (QG == 1 || RG == 1), "tile geometry");
+    static_assert(NBUF == 2 || NBUF == 3, "tile buffers");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    unsigned char* tiles = smem;                                     // [2][BN][STRIDE]
-    float* ring = reinterpret_cast<float*>(smem + 2 * TILE);         // [3][2][BN]: (1-c) tn, tn
-    float* topU = ring + 3 * 2 * GF_BN;                              // [BM][k]
-    int* cnt_l = reinterpret_cast<int*>(topU + GF_BM * a.k);         // [BM] kept rows (this segment)
+    unsigned char* tiles = smem;                                     // [NBUF][TILE]
+    float* ring = reinterpret_cast<float*>(smem + NBUF * TILE);      // [NR][2][BN]: (1-c) tn, tn
+    const int hs = heap_stride(a.k);
+    float* topU = ring + NR * 2 * BN;                                // [BM][hs] max-heaps of U
+    int* cnt_l = reinterpret_cast<int*>(topU + BM * hs);             // [BM] kept rows (this segment)
 
     const int lane = lane_id();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // scalar: uniform DMA branches
@@ -388,9 +454,6 @@ __global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
     const int h = lane >> 5;
     const int qt = blockIdx.x % a.n_qtiles;
     const int seg = blockIdx.x / a.n_qtiles;
-    const int jl = wave * 32 + j;
-    const int64_t q = (int64_t)qt * GF_BM + jl;
-    const bool qvalid = q < a.nq;
     const int64_t row_begin = (int64_t)seg * a.seg_len;
     const int64_t row_end = min(a.nt, row_begin + a.seg_len);
     const int k = a.k;
@@ -400,125 +463,191 @@ __global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
     const int64_t ldb = (int64_t)a.ld_t * sizeof(E);  // train row pitch, bytes
     const unsigned char* trainb = reinterpret_cast<const unsigned char*>(a.train);
 
-    for (int i = threadIdx.x; i < GF_BM * k; i += 256) topU[i] = INF;
-    for (int i = threadIdx.x; i < 3 * 2 * GF_BN; i += 256) ring[i] = INF;
-    if (threadIdx.x < GF_BM) cnt_l[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < BM * hs; i += NT) {
+        const int e = i % hs;
+        topU[i] = (e >= 1 && e <= k) ? INF : -INF;
+    }
+    for (int i = threadIdx.x; i < NR * 2 * BN; i += NT) ring[i] = INF;
+    for (int i = threadIdx.x; i < BM; i += NT) cnt_l[i] = 0;
 
-    uint4 qf[NS];
-    {
+    // per query group g: this lane's query (local jl[g], global q[g]) and its state
+    int jl[QG];
+    int64_t q[QG];
+    bool qvalid[QG];
+    float qn[QG], thr[QG], published[QG], tf[QG];
+    auto make_tf = [&](int g, float th) -> float {
+        if (!qvalid[g]) return -INF;
+        const float m = 0x1p-16f * (fabsf(th) + qn[g] + tnmax);
+        return ((th - c1 * qn[g]) + eta) + m;
+    };
+    uint4 qf[QG][NS];
+#pragma unroll
+    for (int g = 0; g < QG; g++) {
+        jl[g] = wave * 32 * QG + 32 * g + j;
+        q[g] = (int64_t)qt * BM + jl[g];
+        qvalid[g] = q[g] < a.nq;
         const unsigned char* qrow = reinterpret_cast<const unsigned char*>(a.test) +
-                                    (qvalid ? q : 0) * (int64_t)a.ld_q * (int64_t)sizeof(E);
+                                    (qvalid[g] ? q[g] : 0) * (int64_t)a.ld_q * (int64_t)sizeof(E);
 #pragma unroll
         for (int s = 0; s < NS; s++)
-            qf[s] = qvalid ? *reinterpret_cast<const uint4*>(qrow + 32 * s + 16 * h) : make_uint4(0u, 0u, 0u, 0u);
+            qf[g][s] = qvalid[g] ? *reinterpret_cast<const uint4*>(qrow + 32 * s + 16 * h)
+                                 : make_uint4(0u, 0u, 0u, 0u);
+        qn[g] = qvalid[g] ? a.qnorm[q[g]] : 0.0f;
+        thr[g] = qvalid[g] ? o2f(a.gthr[q[g]]) : -INF;
+        published[g] = thr[g];
+        tf[g] = make_tf(g, thr[g]);
     }
-    const float qn = qvalid ? a.qnorm[q] : 0.0f;
-    float thr = qvalid ? o2f(a.gthr[q]) : -INF;
-    float published = thr;
-    auto make_tf = [&](float th) -> float {
-        if (!qvalid) return -INF;
-        const float m = 0x1p-16f * (fabsf(th) + qn + tnmax);
-        return ((th - c1 * qn) + eta) + m;
-    };
-    float tf = make_tf(thr);
 
     // LDS-DMA of one tile: slot P (16 B) of the padded image -> row P / SLOTS, slot P % SLOTS;
-    // the pad slot (SLOTS-1) gets a duplicate of slot 0.  Rows past nt read row nt-1; their
-    // ring entries are +inf (tnorm/tnp are padded with +inf), so they never pass.
-    // per-lane byte offsets of this thread's DMA slots inside a tile (row*ldb + slot), fixed
-    uint32_t doff[DMA_PER_WAVE];
+    // the pad slot (SLOTS-1) gets a duplicate of slot 0.  The last instruction may be
+    // partial (LAST_LANES active; each buffer has room for a whole one).  Rows past nt read
+    // row nt-1; their ring entries are +inf (tnorm/tnp are padded with +inf): never pass.
+    uint32_t doff[DMA_PER_WAVE];  // per-lane byte offsets of this wave's DMA slots in a tile
 #pragma unroll
     for (int i = 0; i < DMA_PER_WAVE; i++) {
-        const int P = (wave + 4 * i) * 64 + lane;
-        const int row = P / SLOTS, sl = P % SLOTS;
+        const int P = (wave + NW * i) * 64 + lane;
+        const int row = min(P / SLOTS, BN - 1), sl = P % SLOTS;
         doff[i] = (uint32_t)(row * ldb + 16 * (sl == SLOTS - 1 ? 0 : sl));
     }
+    // vector-memory ops this wave issues per tile (its DMA instructions + one norm load)
+    int n_dma_wave = (wave >= NW - 2) ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < DMA_PER_WAVE; i++) n_dma_wave += (wave + NW * i < DMA_INS) ? 1 : 0;
     auto dma_tile = [&](int buf, int slot, int64_t r0) {
-        typedef __attribute__((address_space(3))) void lds_void;
-        typedef __attribute__((address_space(1))) const void gbl_void;
         unsigned char* tile = tiles + buf * TILE;
-        const bool tail = r0 + GF_BN > a.nt;  // block-uniform
-        const unsigned char* base = trainb + r0 * ldb;
+        const unsigned char* base = trainb + r0 * ldb;  // block-uniform (SGPRs)
+        const bool full = r0 + BN <= a.nt;
 #pragma unroll
         for (int i = 0; i < DMA_PER_WAVE; i++) {
-            const int ins = wave + 4 * i;
+            const int ins = wave + NW * i;
             if (ins < DMA_INS) {
-                const unsigned char* src = base + doff[i];
-                if (tail) {  // rows past nt re-read row nt-1 (their ring entries are +inf)
+                if (ins == DMA_INS - 1 && lane >= FT::LAST_LANES) continue;
+                if (full) {
+                    dma16s(doff[i], base, lds_addr(tile + ins * 1024));
+                } else {
                     const int P = ins * 64 + lane;
                     const int row = P / SLOTS, sl = P % SLOTS;
                     const int64_t t = min(r0 + row, a.nt - 1);
-                    src = trainb + t * ldb + 16 * (sl == SLOTS - 1 ? 0 : sl);
+                    dma16(trainb + t * ldb + 16 * (sl == SLOTS - 1 ? 0 : sl), lds_addr(tile + ins * 1024));
                 }
-                __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(tile + ins * 1024), 16, 0, 0);
             }
         }
-        float* rs = ring + slot * 2 * GF_BN;
-        if (wave == 2)
-            __builtin_amdgcn_global_load_lds((gbl_void*)(a.tnp + r0 + lane), (lds_void*)rs, 4, 0, 0);
-        else if (wave == 3)
-            __builtin_amdgcn_global_load_lds((gbl_void*)(a.tnorm + r0 + lane), (lds_void*)(rs + GF_BN), 4, 0, 0);
+        float* rs = ring + slot * 2 * BN;
+        if (lane < BN) {
+            if (wave == NW - 2)
+                dma4s(4u * lane, a.tnp + r0, lds_addr(rs));
+            else if (wave == NW - 1)
+                dma4s(4u * lane, a.tnorm + r0, lds_addr(rs + BN));
+        }
     };
 
+    // accumulator a <-> (row group, query group)
+    auto rg_of = [](int acc) { return RG == 2 ? acc : 0; };
+    auto qg_of = [](int acc) { return QG == 2 ? acc : 0; };
+
     // MFMAs of one tile into X, interleaved with the fast test of the previous tile (Y)
-    auto step = [&](floatx16 (&X)[2], floatx16 (&Y)[2], int buf, int slotY) -> bool {
+    auto step = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int buf, int slotY) -> bool {
         const unsigned char* tile = tiles + buf * TILE;
         const unsigned char* a0p = tile + j * STRIDE + 16 * h;
-        const unsigned char* a1p = tile + (32 + j) * STRIDE + 16 * h;
-        const float* tnpY = ring + slotY * 2 * GF_BN;
-        X[0] = floatx16{};
-        X[1] = floatx16{};
-        bool any = false;
-        float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        const unsigned char* a1p = tile + ((RG == 2 ? 32 : 0) + j) * STRIDE + 16 * h;
+        const float* tnpY = ring + slotY * 2 * BN;
 #pragma unroll
-        for (int s = 0; s < NS; s++) {
-            const uint4 x0 = *reinterpret_cast<const uint4*>(a0p + 32 * s);
-            const uint4 x1 = *reinterpret_cast<const uint4*>(a1p + 32 * s);
-            if constexpr (BF) {
-                const bf16x8 b = __builtin_bit_cast(bf16x8, qf[s]);
-                X[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, x0), b, X[0], 0, 0, 0);
-                X[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, x1), b, X[1], 0, 0, 0);
-            } else {
+        for (int c = 0; c < NACC; c++) X[c] = floatx16{};
+        float4 t4[RG];  // norm terms of the rows in use, per row group
+#pragma unroll
+        for (int r = 0; r < RG; r++) t4[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+        float mn[NACC];  // min over this lane's fast-test values per accumulator
+#pragma unroll
+        for (int c = 0; c < NACC; c++) mn[c] = INF;
+        // fast-test values v = 16 acc + reg; QG = 2: both accumulators share the rows
+        auto epi_y = [&](int v) -> float {
+            const int acc = v >> 4, reg = v & 15, ta = rg_of(acc);
+            if ((reg & 3) == 0 && (RG == 2 || acc == 0))
+                t4[ta] = *reinterpret_cast<const float4*>(tnpY + 32 * ta + 8 * (reg >> 2) + 4 * h);
+            return fmaf(-2.0f, Y[acc][reg], f4get(t4[ta], reg & 3));
+        };
+        if constexpr (BF) {
+            // one 32x32x16 MFMA per 16-B fragment: prefetch the A fragments PF k-steps ahead
+            // and interleave the previous tile's fast test between the MFMAs
+            constexpr int PF = 2;
+            uint4 xa[NS], xb[NS];
+#pragma unroll
+            for (int s = 0; s < PF && s < NS; s++) {
+                xa[s] = *reinterpret_cast<const uint4*>(a0p + 32 * s);
+                if (RG == 2) xb[s] = *reinterpret_cast<const uint4*>(a1p + 32 * s);
+            }
+#pragma unroll
+            for (int s = 0; s < NS; s++) {
+                if (s + PF < NS) {
+                    xa[s + PF] = *reinterpret_cast<const uint4*>(a0p + 32 * (s + PF));
+                    if (RG == 2) xb[s + PF] = *reinterpret_cast<const uint4*>(a1p + 32 * (s + PF));
+                }
+#pragma unroll
+                for (int c = 0; c < NACC; c++) {
+                    const bf16x8 A = __builtin_bit_cast(bf16x8, (RG == 2 && c) ? xb[s] : xa[s]);
+                    const bf16x8 B = __builtin_bit_cast(bf16x8, qf[qg_of(c)][s]);
+                    X[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B, X[c], 0, 0, 0);
+#pragma unroll
+                    for (int vv = 0; vv < VPS; vv++) {
+#ifndef KNN_ABLATE_NO_EPI
+                        const float y = epi_y(16 * c + s * VPS + vv);
+                        asm volatile("" ::"v"(y));  // computed here, beside this MFMA
+                        mn[c] = fminf(mn[c], y);
+#else
+                        asm volatile("" ::"v"(Y[c][(s * VPS + vv) & 15]));
+#endif
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);  // keep this k-step's order (prefetch, MFMA, VALU)
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < NS; s++) {
+                const uint4 x0 = *reinterpret_cast<const uint4*>(a0p + 32 * s);
+                const uint4 x1 = RG == 2 ? *reinterpret_cast<const uint4*>(a1p + 32 * s) : x0;
 #pragma unroll
                 for (int jj = 0; jj < 4; jj++) {
-                    X[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(u4getf(x0, jj), u4getf(qf[s], jj), X[0], 0, 0, 0);
-                    X[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(u4getf(x1, jj), u4getf(qf[s], jj), X[1], 0, 0, 0);
-                }
-            }
 #pragma unroll
-            for (int vv = 0; vv < VPG; vv++) {
-                const int v = s * VPG + vv, rb = v >> 4, reg = v & 15;
-                if ((reg & 3) == 0)
-                    t4 = *reinterpret_cast<const float4*>(tnpY + 32 * rb + 8 * (reg >> 2) + 4 * h);
+                    for (int c = 0; c < NACC; c++)
+                        X[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(u4getf((RG == 2 && c) ? x1 : x0, jj),
+                                                                    u4getf(qf[qg_of(c)][s], jj), X[c], 0, 0, 0);
+                }
+#pragma unroll
+                for (int c = 0; c < NACC; c++)
+#pragma unroll
+                    for (int vv = 0; vv < VPS; vv++) {
 #ifndef KNN_ABLATE_NO_EPI
-                const float y = fmaf(-2.0f, Y[rb][reg], f4get(t4, reg & 3));
-                any |= (y <= tf);
+                        mn[c] = fminf(mn[c], epi_y(16 * c + s * VPS + vv));
 #else
-                asm volatile("" ::"v"(Y[rb][reg]), "v"(t4.x));
+                        asm volatile("" ::"v"(Y[c][(s * VPS + vv) & 15]));
 #endif
+                    }
             }
         }
+        bool any = false;
+#pragma unroll
+        for (int c = 0; c < NACC; c++) any |= mn[c] <= tf[qg_of(c)];
         return __ballot(any) != 0ull;
     };
 
     // exact re-check of tile tp (accumulators Y) for the values whose fast test passed:
     // a bit-mask pass, then a wave-uniform loop over the set bits (the value is picked by
     // a select chain, so the accumulators are never indexed dynamically)
-    auto slow = [&](floatx16 (&Y)[2], int tp) {
-        const int64_t r0p = row_begin + (int64_t)tp * GF_BN;
-        const float* tnpY = ring + (tp % 3) * 2 * GF_BN;
-        const float* tnY = tnpY + GF_BN;
+    auto slow = [&](floatx16 (&Y)[NACC], int tp) {
+        const int64_t r0p = row_begin + (int64_t)tp * BN;
+        const float* tnpY = ring + (tp % NR) * 2 * BN;
+        const float* tnY = tnpY + BN;
         uint32_t m = 0;  // bit v = value v passed; built high to low with shift-or (no literals)
 #pragma unroll
-        for (int v4 = 7; v4 >= 0; v4--) {
-            const int rb = v4 >> 2, rq = v4 & 3;
-            const float4 t4 = *reinterpret_cast<const float4*>(tnpY + 32 * rb + 8 * rq + 4 * h);
+        for (int v4 = NV / 4 - 1; v4 >= 0; v4--) {
+            const int acc = v4 >> 2, rq = v4 & 3;
+            const float4 t4 = *reinterpret_cast<const float4*>(tnpY + 32 * rg_of(acc) + 8 * rq + 4 * h);
+            const float tfa = tf[qg_of(acc)];
 #pragma unroll
             for (int e = 3; e >= 0; e--)
-                m = (m << 1) | (uint32_t)(fmaf(-2.0f, Y[rb][4 * rq + e], f4get(t4, e)) <= tf);
+                m = (m << 1) | (uint32_t)(fmaf(-2.0f, Y[acc][4 * rq + e], f4get(t4, e)) <= tfa);
         }
-        // the two lanes of a query take turns, so each list has one writer at a time
-        float* list = topU + jl * k;
+        // the two lanes of a query take turns, so each heap has one writer at a time
         for (int hh = 0; hh < 2; hh++) {
             uint32_t mm = (h == hh) ? m : 0u;
             while (__ballot(mm != 0u)) {
@@ -527,32 +656,43 @@ __global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
                     mm &= mm - 1u;
                     float acc = Y[0][0];
 #pragma unroll
-                    for (int v = 1; v < 32; v++) acc = (b == v) ? Y[v >> 4][v & 15] : acc;
-                    const int reg = b & 15;
-                    const int row = 32 * (b >> 4) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-                    const float s = qn + tnY[row];
+                    for (int v = 1; v < NV; v++) acc = (b == v) ? Y[v >> 4][v & 15] : acc;
+                    const int reg = b & 15, g = qg_of(b >> 4);
+                    const int row = 32 * rg_of(b >> 4) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                    const float qng = (QG == 2 && g) ? qn[QG - 1] : qn[0];
+                    const float s = qng + tnY[row];
                     const float G = fmaf(-2.0f, acc, s);
                     const float dl = fmaf(coef, s, eta);
                     const float L = G - dl;
                     const int64_t t = r0p + row;
-                    if (L <= thr && t < row_end) {
+                    float& th = (QG == 2 && g) ? thr[QG - 1] : thr[0];
+                    if (L <= th && t < row_end) {
                         const float U = G + dl;
-                        const int slot = cnt_l[jl];
-                        cnt_l[jl] = slot + 1;
+                        const int jq = (QG == 2 && g) ? jl[QG - 1] : jl[0];
+                        const int64_t qq = (QG == 2 && g) ? q[QG - 1] : q[0];
+                        const int slot = cnt_l[jq];
+                        cnt_l[jq] = slot + 1;
                         if (slot < a.cap_seg) {
-                            const int64_t o = q * (int64_t)a.cap + (int64_t)seg * a.cap_seg + slot;
+                            const int64_t o = qq * (int64_t)a.cap + (int64_t)seg * a.cap_seg + slot;
                             a.cand_idx[o] = (int32_t)t;
                             a.cand_L[o] = L;
                             a.cand_U[o] = U;
                         }
-                        if (U < list[k - 1]) {
-                            int p = k - 1;
-                            while (p > 0 && list[p - 1] > U) {
-                                list[p] = list[p - 1];
-                                p--;
+                        float* H = topU + jq * hs;
+                        if (U < H[1]) {  // replace the root (the k-th smallest U), sift down
+                            int i = 1;
+                            for (;;) {
+                                const int c = 2 * i;
+                                if (c > k) break;
+                                const float2 cc = *reinterpret_cast<const float2*>(H + c);
+                                const bool right = cc.y > cc.x;
+                                const float cv = right ? cc.y : cc.x;
+                                if (cv <= U) break;
+                                H[i] = cv;
+                                i = c + (right ? 1 : 0);
                             }
-                            list[p] = U;
-                            thr = fminf(thr, list[k - 1]);
+                            H[i] = U;
+                            th = fminf(th, H[1]);
                         }
                     }
                 }
@@ -560,37 +700,57 @@ __global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
         }
-        if (qvalid) {
-            thr = fminf(thr, list[k - 1]);
-            if (h == 0 && thr < published) {
-                atomicMin(&a.gthr[q], f2o(thr));
-                published = thr;
+#pragma unroll
+        for (int g = 0; g < QG; g++) {
+            if (qvalid[g]) {
+                thr[g] = fminf(thr[g], topU[jl[g] * hs + 1]);
+                if (h == 0 && thr[g] < published[g]) {
+                    atomicMin(&a.gthr[q[g]], f2o(thr[g]));
+                    published[g] = thr[g];
+                }
+                tf[g] = make_tf(g, thr[g]);
             }
-            tf = make_tf(thr);
         }
     };
 
-    const int ntiles = (row_end > row_begin) ? (int)((row_end - row_begin + GF_BN - 1) / GF_BN) : 0;
-    floatx16 accA[2], accB[2];
-    accA[0] = accA[1] = accB[0] = accB[1] = floatx16{};
+    const int ntiles = (row_end > row_begin) ? (int)((row_end - row_begin + BN - 1) / BN) : 0;
+    floatx16 accA[NACC], accB[NACC];
+#pragma unroll
+    for (int c = 0; c < NACC; c++) accA[c] = accB[c] = floatx16{};
     __syncthreads();  // LDS init above is complete before any DMA lands
-    if (ntiles > 0) dma_tile(0, 0, row_begin);
-    auto iter = [&](floatx16 (&X)[2], floatx16 (&Y)[2], int it) {
-        const int64_t r0 = row_begin + (int64_t)it * GF_BN;
-        if ((it & 15) == 15 && qvalid) {
-            // pick up thresholds published by other segments (no DMA in flight here)
-            const float g = o2f(__hip_atomic_load(&a.gthr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            if (g < thr) { thr = g; tf = make_tf(thr); }
+#pragma unroll
+    for (int p = 0; p < NBUF - 1; p++)
+        if (p < ntiles) dma_tile(p, p, row_begin + (int64_t)p * BN);
+    bool dirty = false;  // this wave issued vector-memory ops after the newest DMA (slow path)
+    auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
+        const int64_t r0 = row_begin + (int64_t)it * BN;
+        if ((it & 63) == 63) {
+            // pick up thresholds published by other segments (the value is waited on here)
+#pragma unroll
+            for (int g = 0; g < QG; g++) {
+                if (qvalid[g]) {
+                    const float gv = o2f(__hip_atomic_load(&a.gthr[q[g]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    if (gv < thr[g]) { thr[g] = gv; tf[g] = make_tf(g, thr[g]); }
+                }
+            }
         }
-        __syncthreads();  // vmcnt(0): tile it landed; every wave is done with buffer (it+1)&1, slot (it+1)%3
+        // tile it landed (NBUF = 3: tile it+1's DMA may stay in flight); every wave is done
+        // with the buffer / ring slot the next DMA overwrites (tile it-1's, read last iteration)
+        const bool keep_next = NBUF == 3 && it + 1 < ntiles && !dirty;
+        wait_dma_barrier(keep_next ? n_dma_wave : 0);
+        dirty = false;
 #ifndef KNN_ABLATE_NO_DMA
-        if (it + 1 < ntiles) dma_tile((it + 1) & 1, (it + 1) % 3, r0 + GF_BN);
+        if (it + NBUF - 1 < ntiles)
+            dma_tile((it + NBUF - 1) % NBUF, (it + NBUF - 1) % NR, r0 + (int64_t)(NBUF - 1) * BN);
 #endif
-        const bool any = step(X, Y, it & 1, (it + 2) % 3);
+        const bool any = step(X, Y, it % NBUF, (it + NR - 1) % NR);
 #ifndef KNN_ABLATE_NO_SLOW
-        if (any && it > 0) slow(Y, it - 1);
+        if (any && it > 0) {
+            slow(Y, it - 1);
+            dirty = true;
+        }
 #else
-        if (any) asm volatile("" ::"v"(Y[0][0]), "v"(Y[1][3]));
+        if (any) asm volatile("" ::"v"(Y[0][0]), "v"(Y[NACC - 1][3]));
 #endif
     };
     for (int it = 0; it < ntiles; it += 2) {
@@ -601,19 +761,21 @@ __global__ __launch_bounds__(256, 2) void k_gemm_filter(GemmFilterArgs a) {
         // drain: the last tile's accumulators are in accA (ntiles odd) or accB (even)
         const int last = ntiles - 1;
         bool any = false;
-        floatx16 (&L)[2] = (last & 1) ? accB : accA;
-        const float* tnpL = ring + (last % 3) * 2 * GF_BN;
+        floatx16 (&L)[NACC] = (last & 1) ? accB : accA;
+        const float* tnpL = ring + (last % NR) * 2 * BN;
 #pragma unroll
-        for (int v = 0; v < 32; v++) {
-            const int rb = v >> 4, reg = v & 15;
-            const int row = 32 * rb + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-            any |= fmaf(-2.0f, L[rb][reg], tnpL[row]) <= tf;
+        for (int v = 0; v < NV; v++) {
+            const int acc = v >> 4, reg = v & 15;
+            const int row = 32 * rg_of(acc) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            any |= fmaf(-2.0f, L[acc][reg], tnpL[row]) <= tf[qg_of(acc)];
         }
         if (__ballot(any)) slow(L, last);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (qvalid && h == 0) a.cnt[(int64_t)seg * a.nq + q] = cnt_l[jl];
+#pragma unroll
+    for (int g = 0; g < QG; g++)
+        if (qvalid[g] && h == 0) a.cnt[(int64_t)seg * a.nq + q[g]] = cnt_l[jl[g]];
 }
 
 // ---------------------------------------------------------------------------------
@@ -877,10 +1039,50 @@ hipError_t knn_launch_row_norms(const void* x, int elem, int64_t n, int ld, int 
     return hipSuccess;
 }
 
-size_t knn_gemm_filter_lds(int row_bytes, int k) {
-    return 2 * (size_t)GF_BN * (row_bytes + 16) + (3 * 2 * GF_BN + (size_t)GF_BM * k) * sizeof(float) +
-           GF_BM * sizeof(int);
+// LDS of one filter block (mirrors FilterTile + the kernel's carve-up)
+static size_t gemm_filter_lds_of(int row_bytes, int k, int nw, int qg, int rg, int nbuf) {
+    const int bn = 32 * rg, bm = 32 * qg * nw;
+    const int ins = (bn * (row_bytes / 16 + 1) + 63) / 64;
+    return (size_t)nbuf * ins * 1024 + ((size_t)(nbuf + 1) * 2 * bn + (size_t)bm * heap_stride(k)) * sizeof(float) +
+           (size_t)bm * sizeof(int);
 }
+
+// Filter plan per (element type, row bytes, k).
+//  fp32 (MFMA-bound, 16x the cycles per FLOP of bf16): 4 waves x 32 queries, 64-row tiles;
+//    two blocks per CU with double-buffered tiles when the LDS allows (one block's barrier /
+//    DMA phase hides under the other's MFMAs), else one block triple-buffered.
+//  bf16: 8 waves x 32 queries (two waves per SIMD hide each other's fast test, slow path and
+//    waits) over 32-row tiles: 256 queries share every staged train byte, so the L2 -> LDS
+//    bytes per FLOP halve; triple-buffered when the LDS allows.  Large k that does not fit
+//    falls back to the fp32 shape.
+// KNN_FILTER_NBUF=2|3 and KNN_FILTER_SHAPE=w8|w4q2|w4 (bf16) force a shape (kernel studies).
+FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k) {
+    const size_t cap = 160 * 1024;
+    const char* env_nb = getenv("KNN_FILTER_NBUF");
+    const char* env_sh = getenv("KNN_FILTER_SHAPE");
+    const int force_nb = env_nb ? atoi(env_nb) : 0;
+    const std::string shape = env_sh ? env_sh : "";
+    auto fits = [&](int nw, int qg, int rg, int nbuf, size_t limit) {
+        return gemm_filter_lds_of(row_bytes, k, nw, qg, rg, nbuf) <= limit;
+    };
+    auto make = [&](int nw, int qg, int rg, int minw, int nbuf) {
+        FilterPlan f{nw, qg, rg, minw, nbuf, 32 * qg * nw, gemm_filter_lds_of(row_bytes, k, nw, qg, rg, nbuf)};
+        return f;
+    };
+    if (elem == ELEM_BF16 && (shape.empty() || shape == "w8")) {
+        if (force_nb != 2 && fits(8, 1, 1, 3, cap)) return make(8, 1, 1, 2, 3);
+        if (force_nb != 3 && fits(8, 1, 1, 2, cap)) return make(8, 1, 1, 2, 2);
+    }
+    if (elem == ELEM_BF16 && shape == "w4q2") {
+        if (force_nb != 2 && fits(4, 2, 1, 3, cap)) return make(4, 2, 1, 1, 3);
+        if (fits(4, 2, 1, 2, cap)) return make(4, 2, 1, 1, 2);
+    }
+    if (force_nb != 3 && fits(4, 1, 2, 2, cap / 2)) return make(4, 1, 2, 2, 2);
+    if (force_nb != 2 && fits(4, 1, 2, 3, cap)) return make(4, 1, 2, 1, 3);
+    return make(4, 1, 2, 1, 2);
+}
+
+size_t knn_gemm_filter_lds(int elem, int row_bytes, int k) { return knn_gemm_filter_plan(elem, row_bytes, k).lds; }
 
 bool knn_gemm_filter_supported(int elem, int row_bytes) {
     (void)elem;
@@ -888,44 +1090,42 @@ bool knn_gemm_filter_supported(int elem, int row_bytes) {
 }
 
 template <typename E, int RB>
-static const void* gemm_filter_fn() { return reinterpret_cast<const void*>(&k_gemm_filter<E, RB>); }
+static const void* gemm_filter_fn(const FilterPlan& f) {
+#define KNN_FILTER_FN(MINW, NBUF, NW, QG, RG) reinterpret_cast<const void*>(&k_gemm_filter<E, RB, MINW, NBUF, NW, QG, RG>)
+    if constexpr (sizeof(E) == 2) {
+        if (f.nw == 8) return f.nbuf == 3 ? KNN_FILTER_FN(2, 3, 8, 1, 1) : KNN_FILTER_FN(2, 2, 8, 1, 1);
+        if (f.qg == 2) return f.nbuf == 3 ? KNN_FILTER_FN(1, 3, 4, 2, 1) : KNN_FILTER_FN(1, 2, 4, 2, 1);
+    }
+    if (f.minw == 2) return KNN_FILTER_FN(2, 2, 4, 1, 2);
+    return f.nbuf == 3 ? KNN_FILTER_FN(1, 3, 4, 1, 2) : KNN_FILTER_FN(1, 2, 4, 1, 2);
+#undef KNN_FILTER_FN
+}
 
-static const void* gemm_filter_ptr(int elem, int row_bytes) {
+static const void* gemm_filter_ptr(int elem, int row_bytes, const FilterPlan& f) {
     if (elem == ELEM_BF16)
-        return row_bytes == 128 ? gemm_filter_fn<bf16_t, 128>()
-             : row_bytes == 256 ? gemm_filter_fn<bf16_t, 256>() : gemm_filter_fn<bf16_t, 512>();
-    return row_bytes == 128 ? gemm_filter_fn<float, 128>()
-         : row_bytes == 256 ? gemm_filter_fn<float, 256>() : gemm_filter_fn<float, 512>();
+        return row_bytes == 128 ? gemm_filter_fn<bf16_t, 128>(f)
+             : row_bytes == 256 ? gemm_filter_fn<bf16_t, 256>(f) : gemm_filter_fn<bf16_t, 512>(f);
+    return row_bytes == 128 ? gemm_filter_fn<float, 128>(f)
+         : row_bytes == 256 ? gemm_filter_fn<float, 256>(f) : gemm_filter_fn<float, 512>(f);
 }
 
 hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks_per_cu) {
     if (!knn_gemm_filter_supported(elem, row_bytes)) return hipErrorInvalidValue;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, gemm_filter_ptr(elem, row_bytes), 256,
-                                                        knn_gemm_filter_lds(row_bytes, k));
-}
-
-template <typename E, int RB>
-static hipError_t launch_gemm_filter_t(const GemmFilterArgs& a, hipStream_t st) {
-    const size_t lds = knn_gemm_filter_lds(RB, a.k);
-    hipLaunchKernelGGL((k_gemm_filter<E, RB>), dim3((unsigned)(a.n_qtiles * a.nseg)), dim3(256), lds, st, a);
-    KNN_LAUNCH_CHECK();
-    return hipSuccess;
+    const FilterPlan f = knn_gemm_filter_plan(elem, row_bytes, k);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, gemm_filter_ptr(elem, row_bytes, f),
+                                                        64 * f.nw, f.lds);
 }
 
 hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st) {
     if (!knn_gemm_filter_supported(elem, row_bytes)) return hipErrorInvalidValue;
-    if (elem == ELEM_BF16) {
-        switch (row_bytes) {
-            case 128: return launch_gemm_filter_t<bf16_t, 128>(a, st);
-            case 256: return launch_gemm_filter_t<bf16_t, 256>(a, st);
-            default: return launch_gemm_filter_t<bf16_t, 512>(a, st);
-        }
-    }
-    switch (row_bytes) {
-        case 128: return launch_gemm_filter_t<float, 128>(a, st);
-        case 256: return launch_gemm_filter_t<float, 256>(a, st);
-        default: return launch_gemm_filter_t<float, 512>(a, st);
-    }
+    const FilterPlan f = knn_gemm_filter_plan(elem, row_bytes, a.k);
+    const void* fn = gemm_filter_ptr(elem, row_bytes, f);
+    void* args[] = {const_cast<GemmFilterArgs*>(&a)};
+    const dim3 grid((unsigned)(a.n_qtiles * a.nseg));
+    hipError_t e = hipLaunchKernel(fn, grid, dim3(64 * f.nw), args, f.lds, st);
+    if (e != hipSuccess) return e;
+    KNN_LAUNCH_CHECK();
+    return hipSuccess;
 }
 
 template <int R, typename E>
