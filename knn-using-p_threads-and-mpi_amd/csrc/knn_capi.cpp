@@ -58,7 +58,7 @@ struct knn_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // device workspace
-    DBuf tnorm, tnp, qnorm, gthr, cnt, cand_idx, cand_L, cand_U, fb_list, ctrl;
+    DBuf tnorm, tnp, qnorm, gthr, cnt, cand_idx, cand_L, cand_U, fb_list, ctrl, timing;
     // host-API staging (device copies of host inputs / outputs)
     DBuf h_train, h_labels, h_test, h_pred, h_dist, h_idx;
     int32_t* ctrl_host = nullptr;  // pinned: [0] status, [1] fallback count
@@ -267,9 +267,25 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     g.gthr = c->gthr.as<uint32_t>();
     g.cnt = c->cnt.as<int32_t>(); g.cand_idx = c->cand_idx.as<int32_t>();
     g.cand_L = c->cand_L.as<float>(); g.cand_U = c->cand_U.as<float>(); g.cap = cap; g.cap_seg = cap / nseg;
+    // kernel studies: KNN_FILTER_TIMING=1 with a -DKNN_FILTER_TIMING build prints the
+    // filter's per-phase shader clocks per wave (wait+barrier, DMA issue, step, slow path)
+    const bool timing = getenv("KNN_FILTER_TIMING") != nullptr;
+    if (timing) {
+        HIP_OR_FAIL(c, c->timing.ensure(8 * sizeof(unsigned long long)));
+        HIP_OR_FAIL(c, hipMemsetAsync(c->timing.p, 0, 8 * sizeof(unsigned long long), st));
+        g.timing = c->timing.as<unsigned long long>();
+    }
     stage_begin(c, st, "gemm_filter");
     HIP_OR_FAIL(c, knn_launch_gemm_filter(g, dtype, rb, st));
     stage_end(c, st);
+    if (timing) {
+        unsigned long long t[8];
+        HIP_OR_FAIL(c, hipMemcpyAsync(t, c->timing.p, sizeof(t), hipMemcpyDeviceToHost, st));
+        HIP_OR_FAIL(c, hipStreamSynchronize(st));
+        const double w = t[4] ? (double)t[4] : 1.0;
+        fprintf(stderr, "[knn filter timing] waves=%llu clocks/wave: wait+barrier %.4g  dma %.4g  step %.4g  slow %.4g\n",
+                t[4], t[0] / w, t[1] / w, t[2] / w, t[3] / w);
+    }
 
     RescoreArgs r{};
     r.train = tr->feat; r.labels = tr->labels; r.ld_t = tr->ld;
@@ -334,7 +350,7 @@ void knn_destroy(knn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (DBuf* b : {&c->tnorm, &c->tnp, &c->qnorm, &c->gthr, &c->cnt, &c->cand_idx, &c->cand_L, &c->cand_U,
-                    &c->fb_list, &c->ctrl, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
+                    &c->fb_list, &c->ctrl, &c->timing, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
                     &c->h_dist, &c->h_idx})
         b->release();
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);

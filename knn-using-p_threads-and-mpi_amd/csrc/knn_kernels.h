@@ -40,6 +40,7 @@ struct GemmFilterArgs {
     int k; int64_t seg_len; int nseg; int n_qtiles;
     float coef; float eta;
     uint32_t* gthr;
+    unsigned long long* timing;  // KNN_FILTER_TIMING builds: per-phase shader clocks (else NULL)
     int32_t* cnt;  // [nseg][nq] kept rows per (segment, query)
     int32_t* cand_idx; float* cand_L; float* cand_U; int cap; int cap_seg;
 };

@@ -368,6 +368,9 @@ __global__ __launch_bounds__(256) void k_row_norms(const E* __restrict__ x, int6
 // list (LDS counter).
 // ---------------------------------------------------------------------------------
 static constexpr int GF_BM1 = 128;  // queries per block per query group
+#ifndef KNN_FILTER_PF
+#define KNN_FILTER_PF 6  // A-fragment prefetch depth in MFMAs (bf16)
+#endif
 
 __device__ __forceinline__ float f4get(const float4& v, int i) {
     return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
@@ -389,8 +392,14 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds) {
 }
 // scalar base + 32-bit per-lane offset (no per-lane 64-bit address math in the loop)
 __device__ __forceinline__ void dma16s(uint32_t voff, const void* sbase, uint32_t lds) {
+#ifdef KNN_DMA_PLAIN  // kernel study only: a plain register load of the same bytes (results invalid)
+    uint4 tmp;
+    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(tmp) : "v"(voff), "s"(sbase) : "memory");
+    (void)lds;
+#else
     asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds)
                  : "memory", "m0");
+#endif
 }
 __device__ __forceinline__ void dma4s(uint32_t voff, const void* sbase, uint32_t lds) {
     asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sbase), "s"(lds)
@@ -513,32 +522,52 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
     int n_dma_wave = (wave >= NW - 2) ? 1 : 0;
 #pragma unroll
     for (int i = 0; i < DMA_PER_WAVE; i++) n_dma_wave += (wave + NW * i < DMA_INS) ? 1 : 0;
-    auto dma_tile = [&](int buf, int slot, int64_t r0) {
-        unsigned char* tile = tiles + buf * TILE;
-        const unsigned char* base = trainb + r0 * ldb;  // block-uniform (SGPRs)
-        const bool full = r0 + BN <= a.nt;
-#pragma unroll
-        for (int i = 0; i < DMA_PER_WAVE; i++) {
+    // DMA piece i < DMA_PER_WAVE: this wave's i-th 1 KiB instruction of the tile; piece
+    // DMA_PER_WAVE: the tile's norm terms (two waves).  The step issues the pieces spread
+    // between its MFMAs: issued as one burst after the barrier, every wave queued behind
+    // the CU's whole tile of DMA issue (measured ~550 clocks per tile) with its MFMAs idle.
+    constexpr int NPIECE = DMA_PER_WAVE + 1;
+    // LDS byte offsets as plain 32-bit SGPR values (one generic -> LDS conversion, here)
+    const uint32_t lds_tiles = __builtin_amdgcn_readfirstlane(lds_addr(tiles));
+    const uint32_t lds_ring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+    // one tile's DMA: uniform source row pointer, LDS buffer / ring offsets, full-tile flag
+    struct DmaTile { const unsigned char* src; uint32_t lds, lring; int64_t r0; bool full; };
+    auto dma_desc = [&](int buf, int slot, int64_t r0) -> DmaTile {
+        return DmaTile{trainb + r0 * ldb, lds_tiles + (uint32_t)(buf * TILE),
+                       lds_ring + (uint32_t)(slot * 2 * BN * 4), r0, r0 + BN <= a.nt};
+    };
+    auto dma_piece = [&](int i, const DmaTile& d) {
+        if (i < DMA_PER_WAVE) {
             const int ins = wave + NW * i;
             if (ins < DMA_INS) {
-                if (ins == DMA_INS - 1 && lane >= FT::LAST_LANES) continue;
-                if (full) {
-                    dma16s(doff[i], base, lds_addr(tile + ins * 1024));
+                if (i == DMA_PER_WAVE - 1 && ins == DMA_INS - 1 && lane >= FT::LAST_LANES) return;
+                const uint32_t dst = d.lds + (uint32_t)ins * 1024u;
+                if (d.full) {
+                    dma16s(doff[i], d.src, dst);
                 } else {
                     const int P = ins * 64 + lane;
                     const int row = P / SLOTS, sl = P % SLOTS;
-                    const int64_t t = min(r0 + row, a.nt - 1);
-                    dma16(trainb + t * ldb + 16 * (sl == SLOTS - 1 ? 0 : sl), lds_addr(tile + ins * 1024));
+                    const int64_t t = min(d.r0 + row, a.nt - 1);
+                    dma16(trainb + t * ldb + 16 * (sl == SLOTS - 1 ? 0 : sl), dst);
                 }
             }
-        }
-        float* rs = ring + slot * 2 * BN;
-        if (lane < BN) {
+        } else if (lane < BN) {
             if (wave == NW - 2)
-                dma4s(4u * lane, a.tnp + r0, lds_addr(rs));
+                dma4s(4u * lane, a.tnp + d.r0, d.lring);
             else if (wave == NW - 1)
-                dma4s(4u * lane, a.tnorm + r0, lds_addr(rs + BN));
+                dma4s(4u * lane, a.tnorm + d.r0, d.lring + BN * 4);
         }
+    };
+    auto dma_tile = [&](int buf, int slot, int64_t r0) {
+        const DmaTile d = dma_desc(buf, slot, r0);
+#pragma unroll
+        for (int i = 0; i < NPIECE; i++) dma_piece(i, d);
+    };
+    // pieces issued at k-step s of a step, spread evenly over the tile's MFMAs
+    auto dma_at = [&](int s, bool on, const DmaTile& d) {
+#pragma unroll
+        for (int i = 0; i < NPIECE; i++)
+            if (on && (i * NS) / NPIECE == s) dma_piece(i, d);
     };
 
     // accumulator a <-> (row group, query group)
@@ -546,7 +575,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
     auto qg_of = [](int acc) { return QG == 2 ? acc : 0; };
 
     // MFMAs of one tile into X, interleaved with the fast test of the previous tile (Y)
-    auto step = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int buf, int slotY) -> bool {
+    auto step = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int buf, int slotY, bool dma_on,
+                    const DmaTile& dd) -> bool {
         const unsigned char* tile = tiles + buf * TILE;
         const unsigned char* a0p = tile + j * STRIDE + 16 * h;
         const unsigned char* a1p = tile + ((RG == 2 ? 32 : 0) + j) * STRIDE + 16 * h;
@@ -569,7 +599,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
         if constexpr (BF) {
             // one 32x32x16 MFMA per 16-B fragment: prefetch the A fragments PF k-steps ahead
             // and interleave the previous tile's fast test between the MFMAs
-            constexpr int PF = 2;
+            constexpr int PF = KNN_FILTER_PF / NACC;  // covers ~KNN_FILTER_PF x 32 MFMA cycles of LDS latency
             uint4 xa[NS], xb[NS];
 #pragma unroll
             for (int s = 0; s < PF && s < NS; s++) {
@@ -578,6 +608,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
             }
 #pragma unroll
             for (int s = 0; s < NS; s++) {
+                dma_at(s, dma_on, dd);
                 if (s + PF < NS) {
                     xa[s + PF] = *reinterpret_cast<const uint4*>(a0p + 32 * (s + PF));
                     if (RG == 2) xb[s + PF] = *reinterpret_cast<const uint4*>(a1p + 32 * (s + PF));
@@ -603,6 +634,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
         } else {
 #pragma unroll
             for (int s = 0; s < NS; s++) {
+                dma_at(s, dma_on, dd);
                 const uint4 x0 = *reinterpret_cast<const uint4*>(a0p + 32 * s);
                 const uint4 x1 = RG == 2 ? *reinterpret_cast<const uint4*>(a1p + 32 * s) : x0;
 #pragma unroll
@@ -722,6 +754,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
     for (int p = 0; p < NBUF - 1; p++)
         if (p < ntiles) dma_tile(p, p, row_begin + (int64_t)p * BN);
     bool dirty = false;  // this wave issued vector-memory ops after the newest DMA (slow path)
+#ifdef KNN_FILTER_TIMING
+    // per-phase shader clocks of this wave: [0] wait+barrier, [1] DMA issue, [2] step, [3] slow
+    unsigned long long tph[4] = {0, 0, 0, 0};
+#define KNN_TSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define KNN_TSTAMP(v)
+#endif
     auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
         const int64_t r0 = row_begin + (int64_t)it * BN;
         if ((it & 63) == 63) {
@@ -737,13 +776,19 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
         // tile it landed (NBUF = 3: tile it+1's DMA may stay in flight); every wave is done
         // with the buffer / ring slot the next DMA overwrites (tile it-1's, read last iteration)
         const bool keep_next = NBUF == 3 && it + 1 < ntiles && !dirty;
+        KNN_TSTAMP(t0);
         wait_dma_barrier(keep_next ? n_dma_wave : 0);
         dirty = false;
+        KNN_TSTAMP(t1);
 #ifndef KNN_ABLATE_NO_DMA
-        if (it + NBUF - 1 < ntiles)
-            dma_tile((it + NBUF - 1) % NBUF, (it + NBUF - 1) % NR, r0 + (int64_t)(NBUF - 1) * BN);
+        const bool dma_on = it + NBUF - 1 < ntiles;
+#else
+        const bool dma_on = false;
 #endif
-        const bool any = step(X, Y, it % NBUF, (it + NR - 1) % NR);
+        KNN_TSTAMP(t2);
+        const DmaTile dd = dma_desc((it + NBUF - 1) % NBUF, (it + NBUF - 1) % NR, r0 + (int64_t)(NBUF - 1) * BN);
+        const bool any = step(X, Y, it % NBUF, (it + NR - 1) % NR, dma_on, dd);
+        KNN_TSTAMP(t3);
 #ifndef KNN_ABLATE_NO_SLOW
         if (any && it > 0) {
             slow(Y, it - 1);
@@ -751,6 +796,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
         }
 #else
         if (any) asm volatile("" ::"v"(Y[0][0]), "v"(Y[NACC - 1][3]));
+#endif
+#ifdef KNN_FILTER_TIMING
+        KNN_TSTAMP(t4);
+        tph[0] += t1 - t0; tph[1] += t2 - t1; tph[2] += t3 - t2; tph[3] += t4 - t3;
 #endif
     };
     for (int it = 0; it < ntiles; it += 2) {
@@ -776,6 +825,14 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 #pragma unroll
     for (int g = 0; g < QG; g++)
         if (qvalid[g] && h == 0) a.cnt[(int64_t)seg * a.nq + q[g]] = cnt_l[jl[g]];
+#ifdef KNN_FILTER_TIMING
+    if (a.timing && lane == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) atomicAdd(&a.timing[i], tph[i]);
+        atomicAdd(&a.timing[4], 1ull);
+    }
+#endif
+#undef KNN_TSTAMP
 }
 
 // ---------------------------------------------------------------------------------
