@@ -185,6 +185,24 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     stats = ctx.stats()
+    # select stage (k_rescore): one untimed diagnostic pass counts the filter's candidates,
+    # giving the rescore's algorithmic bytes (select stage vs HBM)
+    select = None
+    if rank == 0 and "rescore" in stage_sum:
+        ctx.close()
+        ctx = knn.Context(local, algo=args.algo, train_splits=args.splits, profile=2)
+        step()
+        cand = ctx.stats()["candidates"]
+        esz = 2 if dtype == "bf16" else 4
+        nseg = max(1, stats["train_segments"])
+        resc_ms = stage_sum["rescore"] / args.steps
+        # cnt words + (idx, L, U) per candidate + the query row + k exact rows (a lower
+        # bound on the survivors) + k labels + the prediction
+        byts = 4 * nseg * nq + 12 * cand + nq * d * esz + nq * k * (d * esz + 4) + 4 * nq
+        select = {"kernel": "k_rescore", "bound": "hbm", "avg_launch_ms": round(resc_ms, 3),
+                  "candidates_per_query": round(cand / nq, 1), "algorithmic_bytes": byts,
+                  "achieved": round(byts / (resc_ms * 1e-3) / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
+                  "frac": round(byts / (resc_ms * 1e-3) / 1e9 / 8000.0, 4)}
     total_q = nq_cfg * world if scaling == "weak" else nq_cfg
     gathered = None
     if world > 1:  # outside the timed region: rank 0 collects predictions (mpi.cpp:186)
@@ -226,6 +244,7 @@ def main():
             "predictions_gathered": gathered,
             "roofline": roof,
             "cpu_baseline": cpu,
+            "select_stage": select,
         }
         print(json.dumps(out), flush=True)
     ctx.close()

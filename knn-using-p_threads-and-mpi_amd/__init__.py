@@ -227,7 +227,8 @@ class Context:
 
     def __init__(self, device=0, algo="auto", train_splits=0, profile=False):
         self.lib = load_library()
-        opts = knn_opts(device, ALGOS[algo], train_splits, 1 if profile else 0)
+        # profile: False/0 off, True/1 per-stage HIP events, 2 = also count filter candidates
+        opts = knn_opts(device, ALGOS[algo], train_splits, int(profile))
         h = ctypes.c_void_p()
         st = self.lib.knn_create(ctypes.byref(h), ctypes.byref(opts))
         if st != KNN_OK:

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Profile bench.py workload A on one MI355X (run on the GPU box via gpurun):
+# Profile bench.py (workload A, or BENCH_ARGS="--config C1 ...") on one MI355X (run on the GPU box via gpurun):
 #   1. rocprofv3 --kernel-trace --stats           -> per-kernel average durations
 #   2. rocprofv3 --pmc FETCH_SIZE                 -> HBM read bytes   (own pass)
 #   3. rocprofv3 --pmc WRITE_SIZE                 -> HBM write bytes  (own pass)
@@ -12,7 +12,7 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 STEPS=${STEPS:-2}
 cd /tmp && export TMPDIR=/tmp
 OUT=$R/gpurun_out
-BENCH="$R/bench.py --steps $STEPS --warmup 1 --no-cpu-baseline"
+BENCH="$R/bench.py --steps $STEPS --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_trace -o run \
     -- python3 $BENCH > $OUT/prof_trace.log 2>&1 || { echo "trace pass failed"; exit 1; }

@@ -1,6 +1,6 @@
 """Summarise the rocprofv3 outputs of scripts/profile_bench.sh into profiles/.
 
-    python scripts/summarize_profile.py TAG [gpurun_out]
+    python scripts/summarize_profile.py TAG [gpurun_out] [CONFIG]
 
 Writes profiles/TAG_kernel_stats.csv (the --stats summary as produced),
 profiles/TAG_pmc_traffic.json (per-launch HBM bytes of k_gemm_filter with the gfx950
@@ -53,9 +53,10 @@ def main():
     def mean(xs):
         return sum(xs) / len(xs) if xs else None
 
-    out = {"tag": tag}
+    # the bench workload these counters were taken on (bench.py pmc_traffic(config))
+    out = {"tag": tag, "config": sys.argv[3] if len(sys.argv) > 3 else "A"}
     for k, c in counters.items():
-        if not k.startswith("void k_gemm_filter"):
+        if "k_gemm_filter" not in k:
             continue
         fetch = mean([v for v, _ in c.get("FETCH_SIZE", [])])
         write = mean([v for v, _ in c.get("WRITE_SIZE", [])])
