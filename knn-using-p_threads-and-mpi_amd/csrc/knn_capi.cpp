@@ -201,7 +201,8 @@ int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int
         const double rows = (double)nt / s;
         if (s > 1 && rows < 64 * 64) break;
         const double expect = k * (1.0 + std::log(std::max(rows / k, 1.0))) + 64.0;
-        if (s > 1 && 1.5 * expect > (double)(cap / s)) break;
+        // each lane half of a query fills its own half of the slice with about half the rows
+        if (s > 1 && 1.5 * (0.5 * expect + 32.0) > (double)(cap / s / 2)) break;
         const int64_t w = n_qtiles * s;
         const double eff = (double)w / (double)(((w + slots - 1) / slots) * slots);
         if (eff >= best_eff) { best = s; best_eff = eff; }
@@ -221,7 +222,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     HIP_OR_FAIL(c, c->tnp.ensure(sizeof(float) * (nt + 64)));
     HIP_OR_FAIL(c, c->qnorm.ensure(sizeof(float) * nq));
     HIP_OR_FAIL(c, c->gthr.ensure(sizeof(uint32_t) * nq));
-    HIP_OR_FAIL(c, c->cnt.ensure(sizeof(int32_t) * nq * 8));
+    HIP_OR_FAIL(c, c->cnt.ensure(sizeof(int32_t) * nq * 16));  // [2 * nseg][nq], nseg <= 8
     HIP_OR_FAIL(c, c->cand_idx.ensure(sizeof(int32_t) * nq * cap));
     HIP_OR_FAIL(c, c->cand_L.ensure(sizeof(float) * nq * cap));
     HIP_OR_FAIL(c, c->cand_U.ensure(sizeof(float) * nq * cap));
@@ -271,27 +272,28 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     // filter's per-phase shader clocks per wave (wait+barrier, DMA issue, step, slow path)
     const bool timing = getenv("KNN_FILTER_TIMING") != nullptr;
     if (timing) {
-        HIP_OR_FAIL(c, c->timing.ensure(8 * sizeof(unsigned long long)));
-        HIP_OR_FAIL(c, hipMemsetAsync(c->timing.p, 0, 8 * sizeof(unsigned long long), st));
+        HIP_OR_FAIL(c, c->timing.ensure(16 * sizeof(unsigned long long)));
+        HIP_OR_FAIL(c, hipMemsetAsync(c->timing.p, 0, 16 * sizeof(unsigned long long), st));
         g.timing = c->timing.as<unsigned long long>();
     }
     stage_begin(c, st, "gemm_filter");
     HIP_OR_FAIL(c, knn_launch_gemm_filter(g, dtype, rb, st));
     stage_end(c, st);
     if (timing) {
-        unsigned long long t[8];
+        unsigned long long t[16];
         HIP_OR_FAIL(c, hipMemcpyAsync(t, c->timing.p, sizeof(t), hipMemcpyDeviceToHost, st));
         HIP_OR_FAIL(c, hipStreamSynchronize(st));
         const double w = t[4] ? (double)t[4] : 1.0;
-        fprintf(stderr, "[knn filter timing] waves=%llu clocks/wave: wait+barrier %.4g  dma %.4g  step %.4g  slow %.4g\n",
-                t[4], t[0] / w, t[1] / w, t[2] / w, t[3] / w);
+        fprintf(stderr, "[knn filter timing] waves=%llu clocks/wave: wait+barrier %.4g  dma %.4g  step %.4g  slow %.4g"
+                " (after tile 4096: %.4g; calls %.4g, mask %.4g, turns %.4g)\n", t[4], t[0] / w, t[1] / w,
+                t[2] / w, t[3] / w, t[5] / w, t[6] / w, t[7] / w, t[8] / w);
     }
 
     RescoreArgs r{};
     r.train = tr->feat; r.labels = tr->labels; r.ld_t = tr->ld;
     r.test = te->feat; r.ld_q = te->ld; r.nq = nq; r.d = d; r.k = k; r.C = C; r.elem = dtype;
     r.cnt = g.cnt; r.cand_idx = g.cand_idx; r.cand_L = g.cand_L; r.cand_U = g.cand_U; r.cap = cap;
-    r.nseg = nseg; r.cap_seg = g.cap_seg;
+    r.nseg = 2 * nseg; r.cap_seg = g.cap_seg / 2;  // sub-slices: (segment, lane half)
     r.out = out; r.status = c->ctrl.as<int32_t>();
     r.fb_list = c->fb_list.as<int32_t>(); r.fb_count = c->ctrl.as<int32_t>() + 1;
     stage_begin(c, st, "rescore");
@@ -405,7 +407,7 @@ knn_status predict_core(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te
     c->stats[1] = c->ctrl_host[1];
     if (c->profile >= 2 && algo == KNN_ALGO_GEMM) {
         // diagnostic only: total candidates kept by the filter
-        std::vector<int32_t> h(te->n * c->stats[2]);
+        std::vector<int32_t> h(te->n * 2 * c->stats[2]);
         if (hipMemcpy(h.data(), c->cnt.p, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost) == hipSuccess) {
             int64_t tot = 0;
             for (int32_t v : h) tot += v;

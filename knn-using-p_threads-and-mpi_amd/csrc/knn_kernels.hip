@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256) void k_exact_scan(ExactScanArgs a) {
     int* counts = reinterpret_cast<int*>(smem + a.q_lds_bytes + 4 * 64 * R * sizeof(u64));
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
-#if defined(KNN_ABLATE_NO_SLOW) || defined(KNN_ABLATE_NO_EPI) || defined(KNN_ABLATE_NO_DMA)
+#if defined(KNN_ABLATE_NO_SLOW) || defined(KNN_ABLATE_NO_EPI) || defined(KNN_ABLATE_NO_DMA) || defined(KNN_STUDY_NO_STORE)
     if (a.qlist) return;  // ablation builds time the filter only: skip the fallback scan
 #endif
     const int64_t n_work = a.qlist ? (int64_t)(*a.qcount) : a.nq;
@@ -418,9 +418,9 @@ __device__ __forceinline__ void wait_dma_barrier(int n) {
 #undef KNN_WAIT_CASE
 }
 
-// per-query heap stride in floats: slot 0 unused, heap in [1, k], slots past k hold -inf
-// (so a sibling pair H[2i], H[2i+1] is one aligned 8-byte read)
-__host__ __device__ __forceinline__ int heap_stride(int k) { return (k + 2) & ~1; }
+// per-query 4-ary heap stride in floats: node n >= 1 in slot n-1, the root in the last slot;
+// slots of nodes >= k hold -inf up to the last child group a parent < k reads (slot k+1)
+__host__ __device__ __forceinline__ int heap_stride(int k) { return (k + 3 + 3) & ~3; }
 
 // tile geometry shared by the kernel and the host's LDS sizing: NW waves per block,
 // QG 32-query groups per wave, RG 32-row groups per tile; NACC = QG * RG accumulators
@@ -455,7 +455,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
     float* ring = reinterpret_cast<float*>(smem + NBUF * TILE);      // [NR][2][BN]: (1-c) tn, tn
     const int hs = heap_stride(a.k);
     float* topU = ring + NR * 2 * BN;                                // [BM][hs] max-heaps of U
-    int* cnt_l = reinterpret_cast<int*>(topU + BM * hs);             // [BM] kept rows (this segment)
+    const int cap_sub = a.cap_seg / 2;  // candidate sub-slice of one lane half (h) of a query
 
     const int lane = lane_id();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // scalar: uniform DMA branches
@@ -474,16 +474,17 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 
     for (int i = threadIdx.x; i < BM * hs; i += NT) {
         const int e = i % hs;
-        topU[i] = (e >= 1 && e <= k) ? INF : -INF;
+        topU[i] = (e == hs - 1 || e <= k - 2) ? INF : -INF;  // root, nodes 1..k-1: +inf
     }
     for (int i = threadIdx.x; i < NR * 2 * BN; i += NT) ring[i] = INF;
-    for (int i = threadIdx.x; i < BM; i += NT) cnt_l[i] = 0;
 
     // per query group g: this lane's query (local jl[g], global q[g]) and its state
     int jl[QG];
     int64_t q[QG];
     bool qvalid[QG];
     float qn[QG], thr[QG], published[QG], tf[QG];
+    float root[QG];    // this query's heap root (k-th smallest U kept so far), mirrored in both lanes
+    int ccnt[QG];      // candidates this lane half kept (its sub-slice fill)
     auto make_tf = [&](int g, float th) -> float {
         if (!qvalid[g]) return -INF;
         const float m = 0x1p-16f * (fabsf(th) + qn[g] + tnmax);
@@ -505,6 +506,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
         thr[g] = qvalid[g] ? o2f(a.gthr[q[g]]) : -INF;
         published[g] = thr[g];
         tf[g] = make_tf(g, thr[g]);
+        root[g] = INF;
+        ccnt[g] = 0;
     }
 
     // LDS-DMA of one tile: slot P (16 B) of the padded image -> row P / SLOTS, slot P % SLOTS;
@@ -665,7 +668,16 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
     // exact re-check of tile tp (accumulators Y) for the values whose fast test passed:
     // a bit-mask pass, then a wave-uniform loop over the set bits (the value is picked by
     // a select chain, so the accumulators are never indexed dynamically)
+#ifdef KNN_FILTER_TIMING
+    // per-phase shader clocks of this wave: [0] wait+barrier, [1] DMA issue, [2] step,
+    // [3] slow, [4] slow after tile 4096, [5] slow invocations, [6] mask, [7] turn loops
+    unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define KNN_TSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define KNN_TSTAMP(v)
+#endif
     auto slow = [&](floatx16 (&Y)[NACC], int tp) {
+        KNN_TSTAMP(ts0);
         const int64_t r0p = row_begin + (int64_t)tp * BN;
         const float* tnpY = ring + (tp % NR) * 2 * BN;
         const float* tnY = tnpY + BN;
@@ -679,64 +691,95 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
             for (int e = 3; e >= 0; e--)
                 m = (m << 1) | (uint32_t)(fmaf(-2.0f, Y[acc][4 * rq + e], f4get(t4, e)) <= tfa);
         }
-        // the two lanes of a query take turns, so each heap has one writer at a time
+        KNN_TSTAMP(ts1);
+        // the two lanes of a query take turns, so each heap has one writer at a time; the
+        // candidate slot counters are per lane (each lane half owns a sub-slice)
         for (int hh = 0; hh < 2; hh++) {
             uint32_t mm = (h == hh) ? m : 0u;
             while (__ballot(mm != 0u)) {
                 if (mm != 0u) {
                     const int b = __builtin_ctz(mm);
                     mm &= mm - 1u;
-                    float acc = Y[0][0];
+                    // value b by a binary select tree on the bits of b (no dynamic indexing)
+                    float lv[NV];
 #pragma unroll
-                    for (int v = 1; v < NV; v++) acc = (b == v) ? Y[v >> 4][v & 15] : acc;
+                    for (int v = 0; v < NV; v++) lv[v] = Y[v >> 4][v & 15];
+#pragma unroll
+                    for (int w = NV / 2, bit = 1; w >= 1; w >>= 1, bit <<= 1) {
+                        const bool hi = (b & bit) != 0;
+#pragma unroll
+                        for (int v = 0; v < w; v++) lv[v] = hi ? lv[2 * v + 1] : lv[2 * v];
+                    }
+                    const float acc = lv[0];
                     const int reg = b & 15, g = qg_of(b >> 4);
                     const int row = 32 * rg_of(b >> 4) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-                    const float qng = (QG == 2 && g) ? qn[QG - 1] : qn[0];
-                    const float s = qng + tnY[row];
+                    const bool g1 = QG == 2 && g;
+                    const float s = (g1 ? qn[QG - 1] : qn[0]) + tnY[row];
                     const float G = fmaf(-2.0f, acc, s);
                     const float dl = fmaf(coef, s, eta);
                     const float L = G - dl;
                     const int64_t t = r0p + row;
-                    float& th = (QG == 2 && g) ? thr[QG - 1] : thr[0];
+                    float& th = g1 ? thr[QG - 1] : thr[0];
                     if (L <= th && t < row_end) {
                         const float U = G + dl;
-                        const int jq = (QG == 2 && g) ? jl[QG - 1] : jl[0];
-                        const int64_t qq = (QG == 2 && g) ? q[QG - 1] : q[0];
-                        const int slot = cnt_l[jq];
-                        cnt_l[jq] = slot + 1;
-                        if (slot < a.cap_seg) {
-                            const int64_t o = qq * (int64_t)a.cap + (int64_t)seg * a.cap_seg + slot;
+                        int& slot = g1 ? ccnt[QG - 1] : ccnt[0];
+#ifndef KNN_STUDY_NO_STORE
+                        if (slot < cap_sub) {
+#else
+                        if (slot < 0) {  // kernel study only: no candidate stores
+#endif
+                            const int64_t qq = g1 ? q[QG - 1] : q[0];
+                            const int64_t o = qq * (int64_t)a.cap + (int64_t)(2 * seg + h) * cap_sub + slot;
                             a.cand_idx[o] = (int32_t)t;
                             a.cand_L[o] = L;
                             a.cand_U[o] = U;
                         }
-                        float* H = topU + jq * hs;
-                        if (U < H[1]) {  // replace the root (the k-th smallest U), sift down
-                            int i = 1;
+                        slot++;
+                        float& rt = g1 ? root[QG - 1] : root[0];
+                        if (U < rt) {
+                            // replace the root (the k-th smallest U) of the 4-ary max-heap, sift down:
+                            // node n >= 1 lives in H[n-1], the root in H[hs-1], so the four children
+                            // 4i+1..4i+4 of node i are one aligned 16-byte read at H[4i]
+                            float* H = topU + (g1 ? jl[QG - 1] : jl[0]) * hs;
+                            int i = 0;
+                            float newroot = U;
                             for (;;) {
-                                const int c = 2 * i;
-                                if (c > k) break;
-                                const float2 cc = *reinterpret_cast<const float2*>(H + c);
-                                const bool right = cc.y > cc.x;
-                                const float cv = right ? cc.y : cc.x;
-                                if (cv <= U) break;
-                                H[i] = cv;
-                                i = c + (right ? 1 : 0);
+                                if (4 * i + 1 > k - 1) break;
+                                const float4 cc = *reinterpret_cast<const float4*>(H + 4 * i);
+                                const float m01 = fmaxf(cc.x, cc.y), m23 = fmaxf(cc.z, cc.w);
+                                const float cm = fmaxf(m01, m23);
+                                if (cm <= U) break;
+                                const int ci = cm == cc.x ? 0 : cm == cc.y ? 1 : cm == cc.z ? 2 : 3;
+                                H[i == 0 ? hs - 1 : i - 1] = cm;
+                                if (i == 0) newroot = cm;
+                                i = 4 * i + 1 + ci;
                             }
-                            H[i] = U;
-                            th = fminf(th, H[1]);
+                            H[i == 0 ? hs - 1 : i - 1] = U;
+                            rt = newroot;
+                            th = fminf(th, rt);
                         }
                     }
                 }
             }
+            // the partner lane of each query takes this turn's root
+#pragma unroll
+            for (int g = 0; g < QG; g++) {
+                const float other = __shfl_xor(root[g], 32);
+                if (h != hh) root[g] = other;
+            }
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
         }
+#ifdef KNN_FILTER_TIMING
+        KNN_TSTAMP(ts2);
+        tph[5] += 1; tph[6] += ts1 - ts0; tph[7] += ts2 - ts1;
+#endif
 #pragma unroll
         for (int g = 0; g < QG; g++) {
             if (qvalid[g]) {
-                thr[g] = fminf(thr[g], topU[jl[g] * hs + 1]);
-                if (h == 0 && thr[g] < published[g]) {
+                thr[g] = fminf(thr[g], root[g]);
+                // publish for the other segments of this query (single segment: nobody reads it)
+                if (a.nseg > 1 && h == 0 && thr[g] < published[g]) {
                     atomicMin(&a.gthr[q[g]], f2o(thr[g]));
                     published[g] = thr[g];
                 }
@@ -753,17 +796,14 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 #pragma unroll
     for (int p = 0; p < NBUF - 1; p++)
         if (p < ntiles) dma_tile(p, p, row_begin + (int64_t)p * BN);
-    bool dirty = false;  // this wave issued vector-memory ops after the newest DMA (slow path)
-#ifdef KNN_FILTER_TIMING
-    // per-phase shader clocks of this wave: [0] wait+barrier, [1] DMA issue, [2] step, [3] slow
-    unsigned long long tph[4] = {0, 0, 0, 0};
-#define KNN_TSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#else
-#define KNN_TSTAMP(v)
-#endif
+    // NBUF = 3 issues the next DMA after the slow path, so the slow path's stores are older
+    // than it and the barrier's counted wait still leaves that DMA in flight (vmcnt retires in
+    // issue order).  NBUF = 2 issues it inside the step: it must land by the next barrier.
+    constexpr bool LATE_DMA = NBUF == 3;
+    bool dirty = false;  // NBUF = 2: this wave issued vector-memory ops after the newest DMA
     auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
         const int64_t r0 = row_begin + (int64_t)it * BN;
-        if ((it & 63) == 63) {
+        if ((it & 63) == 63 && a.nseg > 1) {
             // pick up thresholds published by other segments (the value is waited on here)
 #pragma unroll
             for (int g = 0; g < QG; g++) {
@@ -775,7 +815,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
         }
         // tile it landed (NBUF = 3: tile it+1's DMA may stay in flight); every wave is done
         // with the buffer / ring slot the next DMA overwrites (tile it-1's, read last iteration)
-        const bool keep_next = NBUF == 3 && it + 1 < ntiles && !dirty;
+        const bool keep_next = NBUF == 3 && it + 1 < ntiles && (LATE_DMA || !dirty);
         KNN_TSTAMP(t0);
         wait_dma_barrier(keep_next ? n_dma_wave : 0);
         dirty = false;
@@ -787,7 +827,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 #endif
         KNN_TSTAMP(t2);
         const DmaTile dd = dma_desc((it + NBUF - 1) % NBUF, (it + NBUF - 1) % NR, r0 + (int64_t)(NBUF - 1) * BN);
-        const bool any = step(X, Y, it % NBUF, (it + NR - 1) % NR, dma_on, dd);
+        const bool any = step(X, Y, it % NBUF, (it + NR - 1) % NR, dma_on && !LATE_DMA, dd);
         KNN_TSTAMP(t3);
 #ifndef KNN_ABLATE_NO_SLOW
         if (any && it > 0) {
@@ -797,9 +837,14 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 #else
         if (any) asm volatile("" ::"v"(Y[0][0]), "v"(Y[NACC - 1][3]));
 #endif
+        if (LATE_DMA && dma_on) {
+#pragma unroll
+            for (int i = 0; i < NPIECE; i++) dma_piece(i, dd);
+        }
 #ifdef KNN_FILTER_TIMING
         KNN_TSTAMP(t4);
         tph[0] += t1 - t0; tph[1] += t2 - t1; tph[2] += t3 - t2; tph[3] += t4 - t3;
+        if (it >= 4096) tph[4] += t4 - t3;  // slow path after the first 4096 tiles
 #endif
     };
     for (int it = 0; it < ntiles; it += 2) {
@@ -824,12 +869,20 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int g = 0; g < QG; g++)
-        if (qvalid[g] && h == 0) a.cnt[(int64_t)seg * a.nq + q[g]] = cnt_l[jl[g]];
+#ifndef KNN_STUDY_NO_STORE
+        if (qvalid[g]) a.cnt[(int64_t)(2 * seg + h) * a.nq + q[g]] = ccnt[g];
+#else
+        if (qvalid[g]) a.cnt[(int64_t)(2 * seg + h) * a.nq + q[g]] = 0;  // nothing stored: rescore skips
+#endif
 #ifdef KNN_FILTER_TIMING
     if (a.timing && lane == 0) {
 #pragma unroll
         for (int i = 0; i < 4; i++) atomicAdd(&a.timing[i], tph[i]);
         atomicAdd(&a.timing[4], 1ull);
+        atomicAdd(&a.timing[5], tph[4]);
+        atomicAdd(&a.timing[6], tph[5]);
+        atomicAdd(&a.timing[7], tph[6]);
+        atomicAdd(&a.timing[8], tph[7]);
     }
 #endif
 #undef KNN_TSTAMP
@@ -1100,8 +1153,7 @@ hipError_t knn_launch_row_norms(const void* x, int elem, int64_t n, int ld, int 
 static size_t gemm_filter_lds_of(int row_bytes, int k, int nw, int qg, int rg, int nbuf) {
     const int bn = 32 * rg, bm = 32 * qg * nw;
     const int ins = (bn * (row_bytes / 16 + 1) + 63) / 64;
-    return (size_t)nbuf * ins * 1024 + ((size_t)(nbuf + 1) * 2 * bn + (size_t)bm * heap_stride(k)) * sizeof(float) +
-           (size_t)bm * sizeof(int);
+    return (size_t)nbuf * ins * 1024 + ((size_t)(nbuf + 1) * 2 * bn + (size_t)bm * heap_stride(k)) * sizeof(float);
 }
 
 // Filter plan per (element type, row bytes, k).
