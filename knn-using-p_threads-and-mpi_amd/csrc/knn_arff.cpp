@@ -13,9 +13,17 @@
 //     completely; overflow (inf) fails; anything else stays a STRING value, which the
 //     cross-check then rejects for a NUMERIC attribute
 //   * attribute types: numeric|real, string, date, {nominal}; anything else throws
-// The whole file is read at once (libarff reads one byte per fread call).
+// The whole file is read at once (libarff reads one byte per fread call).  When every
+// attribute is NUMERIC (the KNN case) the data section is parsed by several threads
+// (parse_numeric_parallel): tokens are counted per chunk, a prefix sum gives every
+// token its instance/attribute, and each thread converts its own tokens straight into
+// the [n][na] buffer.  Anything the fast path does not model exactly -- '?', quotes,
+// braces, '%', a ',' that does not directly follow a token (libarff's lexer reads an
+// empty token there and stops), a field that does not parse -- sends the whole data
+// section back to the serial lexer, which reproduces libarff's result or error.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cmath>
 #include <cstdarg>
@@ -106,6 +114,8 @@ enum Tok { T_RELATION, T_ATTRIBUTE, T_DATA, T_NUMERIC, T_STRING, T_DATE, T_BOPEN
 class Lexer {
 public:
     explicit Lexer(std::vector<char>&& buf) : b_(std::move(buf)) {}
+    size_t pos() const { return p_; }
+    const std::vector<char>& buffer() const { return b_; }
     Tok next(std::string& s) {
         if (pend_close_) { pend_close_ = false; s = "}"; return T_BCLOSE; }
         for (;;) {
@@ -163,10 +173,88 @@ private:
     bool pend_close_ = false;
 };
 
+inline bool is_sep(char c) { return c == ' ' || c == '\t' || c == '\n' || c == ','; }
+
+int arff_threads() {
+    if (const char* e = std::getenv("KNN_ARFF_THREADS")) {
+        int t = std::atoi(e);
+        if (t >= 1) return t;
+    }
+    unsigned hw = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(hw, 16u));
+}
+
+// All-NUMERIC data section [beg, end) of b -> P->values/kinds/n.  Returns false (P
+// untouched) when the section holds anything outside the plain grammar "token (',' |
+// whitespace) whitespace*" with every token a number; the caller then runs the lexer.
+bool parse_numeric_parallel(const std::vector<char>& b, size_t beg, ParsedArff* P) {
+    const size_t end = b.size(), na = P->attrs.size();
+    const int T = arff_threads();
+    if (T < 2 || na == 0 || end <= beg) return false;
+    const char* d = b.data();
+    // chunk c owns the tokens that START in [cut[c], cut[c+1])
+    std::vector<size_t> cut(T + 1);
+    for (int c = 0; c <= T; c++) cut[c] = beg + (end - beg) * (size_t)c / (size_t)T;
+    std::vector<int64_t> count(T, 0);
+    std::vector<char> bad(T, 0);
+    auto token_start = [&](size_t i) { return !is_sep(d[i]) && (i == beg || is_sep(d[i - 1])); };
+    auto scan = [&](int c) {
+        int64_t n = 0;
+        for (size_t i = cut[c]; i < cut[c + 1]; i++) {
+            const char ch = d[i];
+            if (ch == '?' || ch == '\'' || ch == '"' || ch == '{' || ch == '}' || ch == '%' || ch == '\0') { bad[c] = 1; return; }
+            if (ch == ',' && (i == beg || is_sep(d[i - 1]))) { bad[c] = 1; return; }
+            if (token_start(i)) n++;
+        }
+        count[c] = n;
+    };
+    {
+        std::vector<std::thread> th;
+        for (int c = 1; c < T; c++) th.emplace_back(scan, c);
+        scan(0);
+        for (auto& t : th) t.join();
+    }
+    for (int c = 0; c < T; c++) if (bad[c]) return false;
+    std::vector<int64_t> first(T + 1, 0);
+    for (int c = 0; c < T; c++) first[c + 1] = first[c] + count[c];
+    const int64_t n = first[T] / (int64_t)na;  // a partial last instance is dropped (libarff)
+    std::vector<float> values((size_t)(n * (int64_t)na));
+    auto conv = [&](int c) {
+        int64_t g = first[c];
+        for (size_t i = cut[c]; i < cut[c + 1] && g < n * (int64_t)na; i++) {
+            if (!token_start(i)) continue;
+            size_t j = i;
+            while (j < end && !is_sep(d[j])) j++;
+            float v;
+            if (!parse_float_like_istream(d + i, j - i, &v)) { bad[c] = 1; return; }
+            values[(size_t)g++] = v;
+            i = j - 1;
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int c = 1; c < T; c++) th.emplace_back(conv, c);
+        conv(0);
+        for (auto& t : th) t.join();
+    }
+    for (int c = 0; c < T; c++) if (bad[c]) return false;
+    P->values = std::move(values);
+    P->kinds.assign(P->values.size(), (uint8_t)K_FLOAT);
+    P->n = n;
+    return true;
+}
+
 std::unique_ptr<ParsedArff> parse_file(const std::string& path) {
     FILE* f = std::fopen(path.c_str(), "rb");
     if (!f) throwf("ArffScanner: failed to open the file '%s'!", path.c_str());
     std::vector<char> buf;
+    if (std::fseek(f, 0, SEEK_END) == 0) {
+        const long sz = std::ftell(f);
+        if (sz > 0) buf.resize((size_t)sz);
+        std::rewind(f);
+    }
+    size_t got = buf.empty() ? 0 : std::fread(buf.data(), 1, buf.size(), f);
+    buf.resize(got);
     char chunk[1 << 16];
     size_t r;
     while ((r = std::fread(chunk, 1, sizeof(chunk), f)) > 0) buf.insert(buf.end(), chunk, chunk + r);
@@ -202,6 +290,9 @@ std::unique_ptr<ParsedArff> parse_file(const std::string& path) {
         P->attrs.push_back(std::move(a));
     }
     const size_t na = P->attrs.size();
+    bool all_numeric = na > 0;
+    for (auto& a : P->attrs) all_numeric = all_numeric && a.type == NUMERIC;
+    if (all_numeric && parse_numeric_parallel(lx.buffer(), lx.pos(), P.get())) return P;
     std::vector<float> rv(na);
     std::vector<uint8_t> rk(na);
     std::vector<std::pair<size_t, std::string>> rs;

@@ -148,3 +148,73 @@ def test_shard_range_rule(knn):
             rs = [knn.shard_range(n, w, r) for r in range(w)]
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
+
+
+# --- multi-threaded ingestion ------------------------------------
+def _read_with_threads(knn, path, threads):
+    old = os.environ.get("KNN_ARFF_THREADS")
+    os.environ["KNN_ARFF_THREADS"] = str(threads)
+    try:
+        return knn.read_arff(path)
+    except knn.KnnError as e:
+        return ("error", str(e))
+    finally:
+        if old is None:
+            del os.environ["KNN_ARFF_THREADS"]
+        else:
+            os.environ["KNN_ARFF_THREADS"] = old
+
+
+def _same(a, b):
+    if isinstance(a[0], str) or isinstance(b[0], str):
+        return isinstance(a[0], str) and isinstance(b[0], str) and a == b
+    return (a[0].view(np.uint32).tobytes() == b[0].view(np.uint32).tobytes()
+            and np.array_equal(a[1], b[1]) and a[2] == b[2])
+
+
+@pytest.mark.parametrize("ds", ["small", "medium", "large"])
+def test_parallel_ingestion_matches_serial_on_datasets(knn, ds):
+    for part in ("train", "test"):
+        path = f"{DATA}/{ds}-{part}.arff"
+        serial = _read_with_threads(knn, path, 1)
+        for t in (2, 3, 7, 16):
+            assert _same(_read_with_threads(knn, path, t), serial), (ds, part, t)
+
+
+@pytest.mark.parametrize("body", [
+    "1,2,0\n3.5,4e2,1\n",                 # plain
+    "1,2,0\r\n3,4,1\r\n",                 # CRLF: '\r' stays in the token (libarff)
+    "1 2 0 3 4 1\n5 6",                   # whitespace separators, partial last instance
+    "1.5x,2,0\n+3,-.5,1\n",               # istream prefix rules
+    "1,2,0\n3,,4,1\n",                    # ',,' -> libarff stops at the empty token
+    "1,2,0\n 3 , 4,1\n",                  # ' ,' -> empty token
+    "1,?,0\n3,4,1\n",                     # missing value
+    "1,2,0\n% comment\n3,4,1\n",          # comment line
+    "1,2,0\n3,'4',1\n",                   # quoted numeric field
+    "1,2,0\n3,abc,1\n",                   # non-numeric field -> error
+    "1,2,0\n3,real,1\n",                  # keyword token in data -> error
+    "1e40,2,0\n3,4,1\n",                  # overflow -> error
+    "\n\n1,2,0\n\n3,4,1",                 # blank lines, no final newline
+])
+def test_parallel_ingestion_matches_serial_on_edge_cases(knn, tmp_path, body):
+    head = "@relation r\n@attribute a numeric\n@attribute b numeric\n@attribute class numeric\n@data\n"
+    p = tmp_path / "x.arff"
+    p.write_text(head + body * 40)
+    serial = _read_with_threads(knn, str(p), 1)
+    for t in (2, 5, 16):
+        assert _same(_read_with_threads(knn, str(p), t), serial), t
+
+
+def test_parallel_ingestion_large_synthetic(knn, oracle, tmp_path):
+    """A 20k x 33 synthetic file in %.9g (round-trips bit-exactly through strtof)."""
+    f, lab = oracle.gen(9, 0, 0, 20000, 32)
+    p = tmp_path / "big.arff"
+    with open(p, "w") as fh:
+        fh.write("@relation big\n" + "".join(f"@attribute a{i} numeric\n" for i in range(32)))
+        fh.write("@attribute class numeric\n@data\n")
+        for r in range(len(f)):
+            fh.write(",".join(f"{v:.9g}" for v in f[r]) + f",{lab[r]}\n")
+    got = _read_with_threads(knn, str(p), 8)
+    assert got[0].view(np.uint32).tobytes() == f.view(np.uint32).tobytes()
+    assert np.array_equal(got[1], lab)
+    assert _same(got, _read_with_threads(knn, str(p), 1))
