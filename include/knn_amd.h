@@ -155,6 +155,15 @@ knn_status knn_confusion_matrix(const int32_t* pred, const int32_t* labels, int6
 /* computeAccuracy (main.cpp:102-112): trace(cm) / n as float. */
 float knn_accuracy(const int32_t* cm, int32_t num_classes, int64_t n);
 
+/* On-device computeConfusionMatrix (main.cpp:87-100) for predictions that stay in HBM:
+ * d_cm (device int32[C*C], overwritten) += 1 at [label][pred] for every query; d_correct
+ * (optional device int64[1]) receives trace(cm), so accuracy = *d_correct / (float)n as in
+ * computeAccuracy (main.cpp:102-112).  KNN_EINVAL if a label or prediction is outside
+ * [0, C) (the reference writes out of bounds there). */
+knn_status knn_confusion_matrix_device(knn_ctx* ctx, const int32_t* d_pred, const int32_t* d_labels,
+                                       int64_t n, int32_t num_classes, int32_t* d_cm,
+                                       int64_t* d_correct, void* hip_stream);
+
 /* ARFF loader (replaces ArffParser::parse, libarff/arff_parser.cpp:23, for the
  * read path): NUMERIC attributes parsed with libarff's istringstream>>float rules.
  * The class is the last attribute. */

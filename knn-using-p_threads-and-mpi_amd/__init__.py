@@ -87,6 +87,7 @@ def load_library(path=LIB_PATH):
         "knn_generate": (I32, [P, P, P, I64, I64, I32, I32, I32, I32, ctypes.c_uint64,
                                ctypes.c_uint32, I32, P]),
         "knn_confusion_matrix": (I32, [P, P, I64, I32, P]),
+        "knn_confusion_matrix_device": (I32, [P, P, P, I64, I32, P, P, P]),
         "knn_accuracy": (F, [P, I32, I64]),
         "knn_arff_open": (I32, [ctypes.c_char_p, ctypes.POINTER(P), ctypes.c_char_p, I32]),
         "knn_arff_shape": (None, [P, ctypes.POINTER(I64), ctypes.POINTER(I32), ctypes.POINTER(I32)]),
@@ -308,6 +309,19 @@ class Context:
             self.h, feat.data_ptr(), None if labels is None else labels.data_ptr(), row0,
             feat.shape[0], d, feat.shape[1], dtype, kind, seed, stream_id, num_classes,
             None if stream is None else ctypes.c_void_p(stream)))
+
+    def confusion_matrix_device(self, pred, labels, num_classes, cm=None, stream=None):
+        """computeConfusionMatrix / computeAccuracy (main.cpp:87-112) on device tensors:
+        returns (cm int32 [C][C] device tensor, accuracy as the reference's float)."""
+        import torch
+        if cm is None:
+            cm = torch.empty((num_classes, num_classes), dtype=torch.int32, device=pred.device)
+        corr = torch.zeros(1, dtype=torch.int64, device=pred.device)
+        self._check(self.lib.knn_confusion_matrix_device(
+            self.h, pred.data_ptr(), labels.data_ptr(), pred.shape[0], num_classes, cm.data_ptr(),
+            corr.data_ptr(), None if stream is None else ctypes.c_void_p(stream)))
+        n = pred.shape[0]
+        return cm, float(np.float32(int(corr.item())) / np.float32(n)) if n else float("nan")
 
     def stage_times(self):
         names = (ctypes.c_char_p * 16)()

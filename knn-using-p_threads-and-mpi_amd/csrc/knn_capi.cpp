@@ -543,6 +543,31 @@ knn_status knn_generate(knn_ctx* c, void* d_feat, int32_t* d_labels, int64_t row
     return KNN_OK;
 }
 
+knn_status knn_confusion_matrix_device(knn_ctx* c, const int32_t* d_pred, const int32_t* d_labels, int64_t n,
+                                       int32_t C, int32_t* d_cm, int64_t* d_correct, void* hip_stream) {
+    if (!c) return KNN_EINVAL;
+    c->err.clear();
+    if (C < 1 || C > 16384 || n < 0 || !d_cm || (n > 0 && (!d_pred || !d_labels)))
+        return fail(c, KNN_EINVAL, "confusion: bad arguments (n=%lld, C=%d)", (long long)n, C);
+    HIP_OR_FAIL(c, hipSetDevice(c->device));
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    c->stages.clear();
+    HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st));
+    HIP_OR_FAIL(c, hipMemsetAsync(d_cm, 0, sizeof(int32_t) * (size_t)C * (size_t)C, st));
+    unsigned long long* corr = reinterpret_cast<unsigned long long*>(d_correct);
+    if (!corr) {
+        HIP_OR_FAIL(c, c->timing.ensure(16 * sizeof(unsigned long long)));  // scratch word
+        corr = c->timing.as<unsigned long long>() + 15;
+    }
+    HIP_OR_FAIL(c, hipMemsetAsync(corr, 0, sizeof(unsigned long long), st));
+    stage_begin(c, st, "confusion");
+    HIP_OR_FAIL(c, knn_launch_confusion(d_pred, d_labels, n, C, d_cm, corr, c->ctrl.as<int32_t>(), st));
+    stage_end(c, st);
+    knn_status s = finish_call(c, st);
+    if (s == KNN_EINVAL) return fail(c, KNN_EINVAL, "a label or prediction is outside [0, num_classes)");
+    return s;
+}
+
 knn_status knn_confusion_matrix(const int32_t* pred, const int32_t* labels, int64_t n, int32_t C, int32_t* cm) {
     if (!cm || C < 1 || n < 0 || (n > 0 && (!pred || !labels))) return KNN_EINVAL;
     std::memset(cm, 0, sizeof(int32_t) * (size_t)C * (size_t)C);

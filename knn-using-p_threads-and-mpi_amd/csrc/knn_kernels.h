@@ -84,3 +84,5 @@ hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks
 hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st);
 hipError_t knn_launch_merge(const MergeArgs& a, hipStream_t st);
 hipError_t knn_launch_generate(const GenerateArgs& a, hipStream_t st);
+hipError_t knn_launch_confusion(const int32_t* pred, const int32_t* labels, int64_t n, int C, int32_t* cm,
+                                unsigned long long* correct, int32_t* status, hipStream_t st);

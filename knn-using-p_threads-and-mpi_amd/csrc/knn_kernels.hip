@@ -29,6 +29,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <string>
 
 #include "knn_kernels.h"
@@ -1096,6 +1097,39 @@ __global__ __launch_bounds__(256) void k_generate(GenerateArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
+// k_confusion: cm[label][pred] += 1 (main.cpp:87-100) and the trace (main.cpp:102-112).
+// Integer counts: blocks privatise a C x C matrix in LDS when it fits (C <= 64), so the
+// global atomics are one per cell per block; labels / predictions outside [0, C) set
+// KNN_STATUS_BAD_LABEL instead of writing out of bounds.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_confusion(const int32_t* __restrict__ pred,
+                                                   const int32_t* __restrict__ labels, int64_t n, int C,
+                                                   int32_t* __restrict__ cm,
+                                                   unsigned long long* __restrict__ correct,
+                                                   int32_t* __restrict__ status) {
+    __shared__ int32_t lcm[64 * 64];
+    const bool priv = C <= 64;
+    if (priv)
+        for (int i = threadIdx.x; i < C * C; i += 256) lcm[i] = 0;
+    __syncthreads();
+    unsigned long long ok = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int t = labels[i], p = pred[i];
+        if (t < 0 || t >= C || p < 0 || p >= C) { atomicOr(status, KNN_STATUS_BAD_LABEL); continue; }
+        ok += (t == p);
+        if (priv) atomicAdd(&lcm[t * C + p], 1);
+        else atomicAdd(&cm[(int64_t)t * C + p], 1);
+    }
+#pragma unroll
+    for (int j = 32; j > 0; j >>= 1) ok += __shfl_xor(ok, j);
+    if ((threadIdx.x & 63) == 0 && ok) atomicAdd(correct, ok);
+    __syncthreads();
+    if (priv)
+        for (int i = threadIdx.x; i < C * C; i += 256)
+            if (lcm[i]) atomicAdd(&cm[i], lcm[i]);
+}
+
+// ---------------------------------------------------------------------------------
 // Launchers (host side)
 // ---------------------------------------------------------------------------------
 #define KNN_LAUNCH_CHECK() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return e_; } while (0)
@@ -1284,6 +1318,15 @@ hipError_t knn_launch_merge(const MergeArgs& a, hipStream_t st) {
         case 8: return launch_merge_r<8>(a, st);
         default: return launch_merge_r<16>(a, st);
     }
+}
+
+hipError_t knn_launch_confusion(const int32_t* pred, const int32_t* labels, int64_t n, int C, int32_t* cm,
+                                unsigned long long* correct, int32_t* status, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_confusion, dim3(grid), dim3(256), 0, st, pred, labels, n, C, cm, correct, status);
+    KNN_LAUNCH_CHECK();
+    return hipSuccess;
 }
 
 hipError_t knn_launch_generate(const GenerateArgs& a, hipStream_t st) {

@@ -178,3 +178,30 @@ def test_full_size_config_a_sampled(knn, oracle):
     assert np.array_equal(dd[qs].view(np.uint32), odist.view(np.uint32))
     assert np.array_equal(p[qs], opred)
     c.close()
+
+
+def test_confusion_matrix_device(knn, ctxs, arff):
+    """computeConfusionMatrix / computeAccuracy (main.cpp:87-112) on device == the host
+    version and the reference's fixtures (large k=5), plus a 1M-query random case."""
+    import torch
+    (tf, tl, C), (qf, ql, Cq) = arff["large"]
+    c = ctxs["auto"]
+    pred = c.predict(tf, tl, qf, 5, C)
+    dp = torch.from_numpy(pred).to("cuda:0")
+    dl = torch.from_numpy(ql).to("cuda:0")
+    cm, acc = c.confusion_matrix_device(dp, dl, Cq)
+    gacc, gcm = golden_cm("large", 5)
+    assert np.array_equal(cm.cpu().numpy(), gcm)
+    assert f"{acc:.4f}" == f"{gacc:.4f}"
+    rng = np.random.default_rng(1)
+    for CC in (10, 300):  # LDS-privatised and global-atomic variants
+        p = rng.integers(0, CC, 1_000_000).astype(np.int32)
+        t = rng.integers(0, CC, 1_000_000).astype(np.int32)
+        cm, acc = c.confusion_matrix_device(torch.from_numpy(p).cuda(), torch.from_numpy(t).cuda(), CC)
+        host = knn.computeConfusionMatrix(p, t, CC)
+        assert np.array_equal(cm.cpu().numpy(), host)
+        assert acc == knn.computeAccuracy(host, len(p))
+    bad = torch.tensor([0, 1, 10], dtype=torch.int32, device="cuda:0")
+    with pytest.raises(knn.KnnError) as e:
+        c.confusion_matrix_device(bad, torch.zeros(3, dtype=torch.int32, device="cuda:0"), 10)
+    assert e.value.status == knn.KNN_EINVAL

@@ -1,0 +1,99 @@
+"""The mpi.cpp contract (mpi.cpp:118-206) of knn-using-p_threads-and-mpi_amd/mpi_driver.py:
+argument handling, the reference's scatter of [start, end) slices, the Gatherv placement,
+and the printed line.  CPU: world-size 2 gloo ranks with the slice classifier supplied by
+the oracle (the checker); GPU: the real driver under torchrun, two ranks on one GPU."""
+import importlib.util
+import io
+import os
+import re
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import DATA, PKG_DIR, REPO, golden_manifest, pred_sha
+
+LINE = re.compile(r"^The (-?\d+)-NN classifier for (\d+) test instances on (\d+) train instances "
+                  r"required (\d+) ms CPU time\. Accuracy was (\d\.\d{4})$")
+
+
+def _driver():
+    spec = importlib.util.spec_from_file_location("knn_mpi_driver", os.path.join(PKG_DIR, "mpi_driver.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _oracle_slice(train, test, k, start, end):
+    from conftest import Oracle
+    if k <= 0:
+        return np.zeros(end - start, np.int32)
+    (tf, tl), (qf, _) = train, test
+    _, pred, _, _ = Oracle().knn(tf, tl, qf, k, int(tl.max()) + 1, q0=start, q1=end, threads=2, topk=False)
+    return pred
+
+
+def _worker(rank, world, port, ds, k, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = io.StringIO()
+    full = _driver().run(["mpi", f"{DATA}/{ds}-train.arff", f"{DATA}/{ds}-test.arff", str(k)],
+                         compute=_oracle_slice, out=out)
+    if rank == 0:
+        q.put((out.getvalue().strip(), pred_sha(full)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ds,k,world", [("large", 5, 2), ("small", 3, 3), ("medium", 1, 2)])
+def test_mpi_contract_gloo(ds, k, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, ds, k, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in ps)
+    line, sha = q.get(timeout=10)
+    m = LINE.match(line)
+    assert m, line
+    assert sha == golden_manifest()[f"{ds}_k{k}"]["sha256"]
+
+
+def test_mpi_usage():
+    out = io.StringIO()
+    assert _driver().run(["mpi", "a"], out=out) == 0
+    assert out.getvalue().strip() == "Usage: mpiexec -np numProcesses ./mpi datasets/train.arff datasets/test.arff k"
+
+
+def test_mpi_strtol():
+    d = _driver()
+    assert [d._c_strtol(s) for s in ("5", " 7x", "-3", "abc", "+4")] == [5, 7, -3, 0, 4]
+
+
+@pytest.mark.gpu
+def test_mpi_driver_torchrun_two_ranks_one_gpu():
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+                        os.path.join(PKG_DIR, "mpi_driver.py"), f"{DATA}/large-train.arff",
+                        f"{DATA}/large-test.arff", "5"], capture_output=True, text=True, env=env,
+                       timeout=300, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("The ")]
+    assert len(lines) == 1, r.stdout
+    m = LINE.match(lines[0])
+    assert m and m.group(5) == "0.9948" and m.group(2) == "1718" and m.group(3) == "30803"
