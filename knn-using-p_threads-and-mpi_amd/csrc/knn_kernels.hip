@@ -369,6 +369,9 @@ __global__ __launch_bounds__(256) void k_row_norms(const E* __restrict__ x, int6
 // list (LDS counter).
 // ---------------------------------------------------------------------------------
 static constexpr int GF_BM1 = 128;  // queries per block per query group
+#ifndef KNN_FILTER_DEFER
+#define KNN_FILTER_DEFER 1  // 8-wave shape: record passing values, flush them every 16 tiles
+#endif
 #ifndef KNN_FILTER_PF
 #define KNN_FILTER_PF 6  // A-fragment prefetch depth in MFMAs (bf16)
 #endif
@@ -388,11 +391,21 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds) {
+    lds = __builtin_amdgcn_readfirstlane(lds);
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(lds)
                  : "memory", "m0");
 }
+// a wave-uniform value the compiler may have kept in VGPRs, as SGPRs
+__device__ __forceinline__ const void* sgpr_ptr(const void* p) {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (const void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
 // scalar base + 32-bit per-lane offset (no per-lane 64-bit address math in the loop)
 __device__ __forceinline__ void dma16s(uint32_t voff, const void* sbase, uint32_t lds) {
+    sbase = sgpr_ptr(sbase);
+    lds = __builtin_amdgcn_readfirstlane(lds);
 #ifdef KNN_DMA_PLAIN  // kernel study only: a plain register load of the same bytes (results invalid)
     uint4 tmp;
     asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(tmp) : "v"(voff), "s"(sbase) : "memory");
@@ -403,6 +416,8 @@ __device__ __forceinline__ void dma16s(uint32_t voff, const void* sbase, uint32_
 #endif
 }
 __device__ __forceinline__ void dma4s(uint32_t voff, const void* sbase, uint32_t lds) {
+    sbase = sgpr_ptr(sbase);
+    lds = __builtin_amdgcn_readfirstlane(lds);
     asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sbase), "s"(lds)
                  : "memory", "m0");
 }
@@ -540,7 +555,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
         return DmaTile{trainb + r0 * ldb, lds_tiles + (uint32_t)(buf * TILE),
                        lds_ring + (uint32_t)(slot * 2 * BN * 4), r0, r0 + BN <= a.nt};
     };
-    auto dma_piece = [&](int i, const DmaTile& d) {
+    auto dma_piece = [&](int i, const DmaTile& d) __attribute__((always_inline)) {
         if (i < DMA_PER_WAVE) {
             const int ins = wave + NW * i;
             if (ins < DMA_INS) {
@@ -562,13 +577,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
                 dma4s(4u * lane, a.tnorm + d.r0, d.lring + BN * 4);
         }
     };
-    auto dma_tile = [&](int buf, int slot, int64_t r0) {
+    auto dma_tile = [&](int buf, int slot, int64_t r0) __attribute__((always_inline)) {
         const DmaTile d = dma_desc(buf, slot, r0);
 #pragma unroll
         for (int i = 0; i < NPIECE; i++) dma_piece(i, d);
     };
     // pieces issued at k-step s of a step, spread evenly over the tile's MFMAs
-    auto dma_at = [&](int s, bool on, const DmaTile& d) {
+    auto dma_at = [&](int s, bool on, const DmaTile& d) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < NPIECE; i++)
             if (on && (i * NS) / NPIECE == s) dma_piece(i, d);
@@ -677,104 +692,59 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 #else
 #define KNN_TSTAMP(v)
 #endif
-    auto slow = [&](floatx16 (&Y)[NACC], int tp) {
-        KNN_TSTAMP(ts0);
-        const int64_t r0p = row_begin + (int64_t)tp * BN;
-        const float* tnpY = ring + (tp % NR) * 2 * BN;
-        const float* tnY = tnpY + BN;
-        uint32_t m = 0;  // bit v = value v passed; built high to low with shift-or (no literals)
-#pragma unroll
-        for (int v4 = NV / 4 - 1; v4 >= 0; v4--) {
-            const int acc = v4 >> 2, rq = v4 & 3;
-            const float4 t4 = *reinterpret_cast<const float4*>(tnpY + 32 * rg_of(acc) + 8 * rq + 4 * h);
-            const float tfa = tf[qg_of(acc)];
-#pragma unroll
-            for (int e = 3; e >= 0; e--)
-                m = (m << 1) | (uint32_t)(fmaf(-2.0f, Y[acc][4 * rq + e], f4get(t4, e)) <= tfa);
-        }
-        KNN_TSTAMP(ts1);
-        // the two lanes of a query take turns, so each heap has one writer at a time; the
-        // candidate slot counters are per lane (each lane half owns a sub-slice)
-        for (int hh = 0; hh < 2; hh++) {
-            uint32_t mm = (h == hh) ? m : 0u;
-            while (__ballot(mm != 0u)) {
-                if (mm != 0u) {
-                    const int b = __builtin_ctz(mm);
-                    mm &= mm - 1u;
-                    // value b by a binary select tree on the bits of b (no dynamic indexing)
-                    float lv[NV];
-#pragma unroll
-                    for (int v = 0; v < NV; v++) lv[v] = Y[v >> 4][v & 15];
-#pragma unroll
-                    for (int w = NV / 2, bit = 1; w >= 1; w >>= 1, bit <<= 1) {
-                        const bool hi = (b & bit) != 0;
-#pragma unroll
-                        for (int v = 0; v < w; v++) lv[v] = hi ? lv[2 * v + 1] : lv[2 * v];
-                    }
-                    const float acc = lv[0];
-                    const int reg = b & 15, g = qg_of(b >> 4);
-                    const int row = 32 * rg_of(b >> 4) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-                    const bool g1 = QG == 2 && g;
-                    const float s = (g1 ? qn[QG - 1] : qn[0]) + tnY[row];
-                    const float G = fmaf(-2.0f, acc, s);
-                    const float dl = fmaf(coef, s, eta);
-                    const float L = G - dl;
-                    const int64_t t = r0p + row;
-                    float& th = g1 ? thr[QG - 1] : thr[0];
-                    if (L <= th && t < row_end) {
-                        const float U = G + dl;
-                        int& slot = g1 ? ccnt[QG - 1] : ccnt[0];
+    // keep candidate (L, U) of global row t for query group g of this lane: the exact test
+    // against the current threshold, the candidate store into this lane half's sub-slice,
+    // and, if U beats the heap root, a sift-down of the 4-ary max-heap (node n >= 1 in
+    // H[n-1], the root in H[hs-1]: the four children 4i+1..4i+4 of node i are one aligned
+    // 16-byte read at H[4i]).  Only one lane of a query may run it at a time.
+    auto accept = [&](float L, float U, int64_t t, bool g1) __attribute__((always_inline)) {
+        float& th = g1 ? thr[QG - 1] : thr[0];
+        if (!(L <= th)) return;
+        int& slot = g1 ? ccnt[QG - 1] : ccnt[0];
 #ifndef KNN_STUDY_NO_STORE
-                        if (slot < cap_sub) {
+        if (slot < cap_sub) {
 #else
-                        if (slot < 0) {  // kernel study only: no candidate stores
+        if (slot < 0) {  // kernel study only: no candidate stores
 #endif
-                            const int64_t qq = g1 ? q[QG - 1] : q[0];
-                            const int64_t o = qq * (int64_t)a.cap + (int64_t)(2 * seg + h) * cap_sub + slot;
-                            a.cand_idx[o] = (int32_t)t;
-                            a.cand_L[o] = L;
-                            a.cand_U[o] = U;
-                        }
-                        slot++;
-                        float& rt = g1 ? root[QG - 1] : root[0];
-                        if (U < rt) {
-                            // replace the root (the k-th smallest U) of the 4-ary max-heap, sift down:
-                            // node n >= 1 lives in H[n-1], the root in H[hs-1], so the four children
-                            // 4i+1..4i+4 of node i are one aligned 16-byte read at H[4i]
-                            float* H = topU + (g1 ? jl[QG - 1] : jl[0]) * hs;
-                            int i = 0;
-                            float newroot = U;
-                            for (;;) {
-                                if (4 * i + 1 > k - 1) break;
-                                const float4 cc = *reinterpret_cast<const float4*>(H + 4 * i);
-                                const float m01 = fmaxf(cc.x, cc.y), m23 = fmaxf(cc.z, cc.w);
-                                const float cm = fmaxf(m01, m23);
-                                if (cm <= U) break;
-                                const int ci = cm == cc.x ? 0 : cm == cc.y ? 1 : cm == cc.z ? 2 : 3;
-                                H[i == 0 ? hs - 1 : i - 1] = cm;
-                                if (i == 0) newroot = cm;
-                                i = 4 * i + 1 + ci;
-                            }
-                            H[i == 0 ? hs - 1 : i - 1] = U;
-                            rt = newroot;
-                            th = fminf(th, rt);
-                        }
-                    }
-                }
-            }
-            // the partner lane of each query takes this turn's root
-#pragma unroll
-            for (int g = 0; g < QG; g++) {
-                const float other = __shfl_xor(root[g], 32);
-                if (h != hh) root[g] = other;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
+            const int64_t qq = g1 ? q[QG - 1] : q[0];
+            const int64_t o = qq * (int64_t)a.cap + (int64_t)(2 * seg + h) * cap_sub + slot;
+            a.cand_idx[o] = (int32_t)t;
+            a.cand_L[o] = L;
+            a.cand_U[o] = U;
         }
-#ifdef KNN_FILTER_TIMING
-        KNN_TSTAMP(ts2);
-        tph[5] += 1; tph[6] += ts1 - ts0; tph[7] += ts2 - ts1;
-#endif
+        slot++;
+        float& rt = g1 ? root[QG - 1] : root[0];
+        if (U < rt) {
+            float* H = topU + (g1 ? jl[QG - 1] : jl[0]) * hs;
+            int i = 0;
+            float newroot = U;
+            for (;;) {
+                if (4 * i + 1 > k - 1) break;
+                const float4 cc = *reinterpret_cast<const float4*>(H + 4 * i);
+                const float m01 = fmaxf(cc.x, cc.y), m23 = fmaxf(cc.z, cc.w);
+                const float cm = fmaxf(m01, m23);
+                if (cm <= U) break;
+                const int ci = cm == cc.x ? 0 : cm == cc.y ? 1 : cm == cc.z ? 2 : 3;
+                H[i == 0 ? hs - 1 : i - 1] = cm;
+                if (i == 0) newroot = cm;
+                i = 4 * i + 1 + ci;
+            }
+            H[i == 0 ? hs - 1 : i - 1] = U;
+            rt = newroot;
+            th = fminf(th, rt);
+        }
+    };
+    // after a round of accepts: the partner lane takes the root, thresholds tighten
+    auto sync_roots = [&](int hh) __attribute__((always_inline)) {
+#pragma unroll
+        for (int g = 0; g < QG; g++) {
+            const float other = __shfl_xor(root[g], 32);
+            if (h != hh) root[g] = other;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    };
+    auto publish = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int g = 0; g < QG; g++) {
             if (qvalid[g]) {
@@ -787,6 +757,125 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
                 tf[g] = make_tf(g, thr[g]);
             }
         }
+    };
+    // fast-test pass bits of tile tp's accumulators Y (bit v = value v)
+    auto pass_mask = [&](floatx16 (&Y)[NACC], int tp) -> uint32_t {
+        const float* tnpY = ring + (tp % NR) * 2 * BN;
+        uint32_t m = 0;  // built high to low with shift-or (no literals)
+#pragma unroll
+        for (int v4 = NV / 4 - 1; v4 >= 0; v4--) {
+            const int acc = v4 >> 2, rq = v4 & 3;
+            const float4 t4 = *reinterpret_cast<const float4*>(tnpY + 32 * rg_of(acc) + 8 * rq + 4 * h);
+            const float tfa = tf[qg_of(acc)];
+#pragma unroll
+            for (int e = 3; e >= 0; e--)
+                m = (m << 1) | (uint32_t)(fmaf(-2.0f, Y[acc][4 * rq + e], f4get(t4, e)) <= tfa);
+        }
+        return m;
+    };
+    // exact (L, U, row) of value b of tile tp (a select tree on the bits of b: the
+    // accumulators are never indexed dynamically)
+    auto value_lu = [&](floatx16 (&Y)[NACC], int tp, int b, float& L, float& U, int64_t& t, bool& g1) {
+        float lv[NV];
+#pragma unroll
+        for (int v = 0; v < NV; v++) lv[v] = Y[v >> 4][v & 15];
+#pragma unroll
+        for (int lvl = 0; (NV >> (lvl + 1)) >= 1; lvl++) {
+            const bool hi = (b >> lvl) & 1;
+#pragma unroll
+            for (int v = 0; v < (NV >> (lvl + 1)); v++) lv[v] = hi ? lv[2 * v + 1] : lv[2 * v];
+        }
+        const int reg = b & 15;
+        const int row = 32 * rg_of(b >> 4) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        g1 = QG == 2 && qg_of(b >> 4);
+        const float s = (g1 ? qn[QG - 1] : qn[0]) + ring[(tp % NR) * 2 * BN + BN + row];
+        const float G = fmaf(-2.0f, lv[0], s);
+        const float dl = fmaf(coef, s, eta);
+        L = G - dl;
+        U = G + dl;
+        const int64_t tt = row_begin + (int64_t)tp * BN + row;
+        t = tt < row_end ? tt : -1;
+    };
+
+    // immediate slow path: every passing value of tile tp is accepted now
+    auto slow = [&](floatx16 (&Y)[NACC], int tp) {
+        KNN_TSTAMP(ts0);
+        const uint32_t m = pass_mask(Y, tp);
+        KNN_TSTAMP(ts1);
+        // the two lanes of a query take turns, so each heap has one writer at a time; the
+        // candidate slot counters are per lane (each lane half owns a sub-slice)
+        for (int hh = 0; hh < 2; hh++) {
+            uint32_t mm = (h == hh) ? m : 0u;
+            while (__ballot(mm != 0u)) {
+                if (mm != 0u) {
+                    const int b = __builtin_ctz(mm);
+                    mm &= mm - 1u;
+                    float L, U;
+                    int64_t t;
+                    bool g1;
+                    value_lu(Y, tp, b, L, U, t, g1);
+                    if (t >= 0) accept(L, U, t, g1);
+                }
+            }
+            sync_roots(hh);
+        }
+#ifdef KNN_FILTER_TIMING
+        KNN_TSTAMP(ts2);
+        tph[5] += 1; tph[6] += ts1 - ts0; tph[7] += ts2 - ts1;
+#endif
+        publish();
+    };
+
+    // deferred slow path (8-wave shape): passing values are only recorded -- exact (L, U,
+    // row) into a small per-lane register queue, no LDS chain, no global stores -- and the
+    // queue is flushed through accept() every DEFER_EVERY tiles by every wave at the same
+    // tile (one wave's heap work then no longer holds the other seven at each barrier),
+    // or at once when some lane's queue is full.  A threshold that waits for the flush is
+    // stale but still valid (it only ever tightens).
+    constexpr int RQ = 4;
+    float qL[RQ], qU[RQ];
+    int qT[RQ];
+    bool qG[RQ];
+    int qcnt = 0;
+#pragma unroll
+    for (int i = 0; i < RQ; i++) { qL[i] = qU[i] = 0.f; qT[i] = 0; qG[i] = false; }
+    auto flush = [&]() __attribute__((always_inline)) {
+        for (int hh = 0; hh < 2; hh++) {
+#pragma unroll
+            for (int i = 0; i < RQ; i++) {
+                const bool mine = h == hh && i < qcnt;
+                if (__ballot(mine) && mine) accept(qL[i], qU[i], (int64_t)qT[i], qG[i]);
+            }
+            sync_roots(hh);
+        }
+        qcnt = 0;
+        publish();
+    };
+    auto record = [&](floatx16 (&Y)[NACC], int tp) {
+        KNN_TSTAMP(ts0);
+        uint32_t mm = pass_mask(Y, tp);
+        KNN_TSTAMP(ts1);
+        while (__ballot(mm != 0u)) {
+            if (__ballot(qcnt >= RQ && mm != 0u)) flush();
+            if (mm != 0u) {
+                const int b = __builtin_ctz(mm);
+                mm &= mm - 1u;
+                float L, U;
+                int64_t t;
+                bool g1;
+                value_lu(Y, tp, b, L, U, t, g1);
+                if (t >= 0 && L <= (g1 ? thr[QG - 1] : thr[0])) {
+#pragma unroll
+                    for (int i = 0; i < RQ; i++)
+                        if (i == qcnt) { qL[i] = L; qU[i] = U; qT[i] = (int)t; qG[i] = g1; }
+                    qcnt++;
+                }
+            }
+        }
+#ifdef KNN_FILTER_TIMING
+        KNN_TSTAMP(ts2);
+        tph[5] += 1; tph[6] += ts1 - ts0; tph[7] += ts2 - ts1;
+#endif
     };
 
     const int ntiles = (row_end > row_begin) ? (int)((row_end - row_begin + BN - 1) / BN) : 0;
@@ -801,6 +890,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
     // than it and the barrier's counted wait still leaves that DMA in flight (vmcnt retires in
     // issue order).  NBUF = 2 issues it inside the step: it must land by the next barrier.
     constexpr bool LATE_DMA = NBUF == 3;
+    constexpr bool DEFER = NW == 8 && KNN_FILTER_DEFER;  // deferred slow path (see record())
+    constexpr int DEFER_EVERY = 16;
     bool dirty = false;  // NBUF = 2: this wave issued vector-memory ops after the newest DMA
     auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
         const int64_t r0 = row_begin + (int64_t)it * BN;
@@ -831,7 +922,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
         const bool any = step(X, Y, it % NBUF, (it + NR - 1) % NR, dma_on && !LATE_DMA, dd);
         KNN_TSTAMP(t3);
 #ifndef KNN_ABLATE_NO_SLOW
-        if (any && it > 0) {
+        if constexpr (DEFER) {
+            if (any && it > 0) record(Y, it - 1);
+            if ((it & (DEFER_EVERY - 1)) == DEFER_EVERY - 1 && __ballot(qcnt > 0)) {
+                flush();
+                dirty = true;
+            }
+        } else if (any && it > 0) {
             slow(Y, it - 1);
             dirty = true;
         }
@@ -855,16 +952,27 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
     if (ntiles > 0) {
         // drain: the last tile's accumulators are in accA (ntiles odd) or accB (even)
         const int last = ntiles - 1;
-        bool any = false;
-        floatx16 (&L)[NACC] = (last & 1) ? accB : accA;
-        const float* tnpL = ring + (last % NR) * 2 * BN;
+        // one static binding per branch: a runtime-selected reference to a register array
+        // would put both accumulator sets in scratch memory
+        auto drain = [&](floatx16 (&L)[NACC]) {
+            bool any = false;
+            const float* tnpL = ring + (last % NR) * 2 * BN;
 #pragma unroll
-        for (int v = 0; v < NV; v++) {
-            const int acc = v >> 4, reg = v & 15;
-            const int row = 32 * rg_of(acc) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-            any |= fmaf(-2.0f, L[acc][reg], tnpL[row]) <= tf[qg_of(acc)];
-        }
-        if (__ballot(any)) slow(L, last);
+            for (int v = 0; v < NV; v++) {
+                const int acc = v >> 4, reg = v & 15;
+                const int row = 32 * rg_of(acc) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                any |= fmaf(-2.0f, L[acc][reg], tnpL[row]) <= tf[qg_of(acc)];
+            }
+            if (__ballot(any)) {
+                if constexpr (DEFER) record(L, last);
+                else slow(L, last);
+            }
+        };
+        if (last & 1) drain(accB);
+        else drain(accA);
+    }
+    if constexpr (DEFER) {
+        if (__ballot(qcnt > 0)) flush();
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
