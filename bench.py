@@ -1,6 +1,6 @@
 """Throughput bench of the KNN hot path (BASELINE.json metric: distance pairs/s).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config A|B|C|C1] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config A|B|C|C1|L] [--no-cpu-baseline]
 
 One process per GPU (torchrun for N > 1).  Workload A (default, BASELINE configs[2]):
 1,000,000 train x 100,000 query rows per GPU x 128-d fp32, k = 10, 10 classes, synthetic
@@ -17,6 +17,12 @@ one all-to-all (RCCL over xGMI) to the rank that owns each query, which merges +
 C1 is one rank's share of C on 8 GPUs (4M train rows x 1M queries), runnable on 1 GPU
 through the same code path.
 
+Config L (BASELINE configs[1]) is the reference's own large ARFF pair (tests/data,
+30,803 train x 1,718 test x 11-d, k = 5) parsed by the boundary's reader, resident in
+HBM, classified by the direct-form path (k_exact_scan); its predictions are compared
+with the golden file captured from the reference (accuracy bit-match), and the CPU
+baseline is the reference's own multi-thread binary (and serial main) on the same files.
+
 Rank 0 prints one JSON line.  roofline: the dominant kernel (k_gemm_filter) timed with
 HIP events on its own stream; cpu_baseline: the reference's pthreads KNN (oracle/_ref,
 built -O0 as shipped) on a bounded sample, else the C restatement labelled "port".
@@ -29,6 +35,8 @@ import subprocess
 import sys
 import time
 
+import numpy as np
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
@@ -38,7 +46,9 @@ CONFIGS = {
     "B": (4_000_000, 1_000_000, 64, 32, 10, 2, "strong", "f32", "test"),
     "C": (32_000_000, 1_000_000, 256, 100, 10, 3, "strong", "bf16", "train"),
     "C1": (4_000_000, 1_000_000, 256, 100, 10, 3, "strong", "bf16", "train"),
+    "L": (30_803, 1_718, 11, 5, 10, 0, "strong", "f32", "arff"),
 }
+ARFF_L = ("tests/data/large-train.arff", "tests/data/large-test.arff", "tests/golden/pred_large_k5.txt")
 METRIC = "distance pairs/sec + queries/sec at 1/2/4/8 GPUs; accuracy bit-match"
 MFMA_PEAK_TFLOPS = {  # MI355X_MICROARCH.md, dense
     "f32": 157.3,    # v_mfma_f32_32x32x2_f32
@@ -71,6 +81,97 @@ def cpu_baseline(d, k, C, seed, kind=0):
     dt = time.perf_counter() - t0
     return {"value": nt_s * nq_s / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
             "sample": sample + "; oracle/knn_oracle.c -O2", "queries_per_s": nq_s / dt}
+
+
+def cpu_baseline_arff(k, threads=None):
+    """The reference binaries themselves (oracle/_ref, -O0 as shipped) on the large ARFF
+    pair: multi-thread.cpp with T threads and serial main.cpp.  They print whole
+    milliseconds of KNN() time (parse excluded, multi-thread.cpp:160-199); median of 3."""
+    import re
+    threads = threads or int(os.environ.get("KNN_BENCH_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    tr, te = (os.path.join(REPO, p) for p in ARFF_L[:2])
+    exe_mt = os.path.join(REPO, "oracle", "_ref", "multi-thread")
+    exe_se = os.path.join(REPO, "oracle", "_ref", "main")
+    if not (os.path.exists(exe_mt) and os.path.exists(exe_se)):
+        return None
+
+    def run(cmd):
+        out = subprocess.run(cmd, capture_output=True, text=True, check=True, timeout=600).stdout
+        return int(re.search(r"required (\d+) ms", out).group(1))
+
+    mt = sorted(run([exe_mt, tr, te, str(k), str(threads)]) for _ in range(3))[1]
+    se = run([exe_se, tr, te, str(k)])
+    pairs = 30_803 * 1_718
+    return {"value": pairs / (mt * 1e-3), "unit": "pairs/s", "cores": threads, "kind": "reference",
+            "sample": f"the whole workload (large ARFF pair, k={k}); reference multi-thread.cpp with "
+                      f"{threads} threads, -O0 as shipped, median of 3 (ms resolution)",
+            "ms": mt, "serial_main_ms": se, "serial_main_pairs_per_s": pairs / (se * 1e-3)}
+
+
+def bench_arff(args, knn, torch, local):
+    """configs[1]: the reference's large ARFF pair, k = 5, inputs resident in HBM."""
+    nt, nq, d, k, C = CONFIGS["L"][:5]
+    tf, tl, _ = knn.read_arff(os.path.join(REPO, ARFF_L[0]))
+    qf, ql, _ = knn.read_arff(os.path.join(REPO, ARFF_L[1]))
+    assert tf.shape == (nt, d) and qf.shape == (nq, d), (tf.shape, qf.shape)
+    C = int(tl.max()) + 1  # train->num_classes() (main.cpp:35)
+    dev = torch.device("cuda", local)
+    ctx = knn.Context(local, algo=args.algo, profile=True)
+    # device rows are 16-B aligned: [n][ld] with ld = 12 for d = 11 (the pad column is never read)
+    ld = (d + 3) // 4 * 4
+    train = torch.zeros((nt, ld), dtype=torch.float32, device=dev)
+    test = torch.zeros((nq, ld), dtype=torch.float32, device=dev)
+    train[:, :d] = torch.from_numpy(tf).to(dev)
+    test[:, :d] = torch.from_numpy(qf).to(dev)
+    labels = torch.from_numpy(tl).to(dev)
+    pred = torch.empty(nq, dtype=torch.int32, device=dev)
+    for _ in range(args.warmup):
+        ctx.predict_device(train, labels, test, k, C, pred, d=d)
+    torch.cuda.synchronize()
+    stage_sum = {}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.predict_device(train, labels, test, k, C, pred, d=d)
+        for name, ms in ctx.stage_times().items():
+            stage_sum[name] = stage_sum.get(name, 0.0) + ms
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    got = pred.cpu().numpy()
+    want = np.loadtxt(os.path.join(REPO, ARFF_L[2]), dtype=np.int32)
+    # host buffers in, predictions out (knn_predict: uploads inside the call, PCIe-inclusive)
+    t1 = time.perf_counter()
+    host_pred = ctx.predict(tf, tl, qf, k, C)
+    host_ms = 1e3 * (time.perf_counter() - t1)
+    cm = knn.computeConfusionMatrix(got, ql, C)
+    pairs = float(nt) * nq * args.steps
+    stages = {n: v / args.steps for n, v in stage_sum.items()}
+    scan = stages.get("exact_scan")
+    roof = None
+    if scan:
+        ops = 3.0 * d * nt * nq  # sub, mul, add per dimension per pair (unfused: the reference's bits)
+        roof = {"bound": "valu", "achieved": round(ops / (scan * 1e-3) / 1e12, 3), "peak": 78.6,
+                "unit": "Tops/s", "frac": round(ops / (scan * 1e-3) / 1e12 / 78.6, 4), "traffic": None,
+                "kernel": "k_exact_scan", "avg_launch_ms": round(scan, 4),
+                "note": "launch/latency bound: 52.9 M pairs is ~22 us of VALU at peak"}
+    out = {
+        "metric": METRIC, "value": pairs / elapsed, "unit": "pairs/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "the reference's large ARFF pair (tests/data), parsed by the boundary's reader",
+        "config": {"workload": f"L: large-train.arff x large-test.arff ({nt} x {nq} x {d}-d), k={k}",
+                   "n_train": nt, "n_query_total": nq, "d": d, "k": k, "classes": C,
+                   "parallelism": "single GPU, direct form"},
+        "queries_per_s": nq * args.steps / elapsed,
+        "stages_ms": {n: round(v, 4) for n, v in stages.items()},
+        "bit_match": {"predictions_equal_reference": bool(np.array_equal(got, want)),
+                      "host_path_equal": bool(np.array_equal(host_pred, want)),
+                      "accuracy": float(np.float32(np.trace(cm)) / np.float32(nq))},
+        "host_buffers_ms": round(host_ms, 3),
+        "roofline": roof,
+        "cpu_baseline": None if args.no_cpu_baseline else cpu_baseline_arff(k),
+    }
+    print(json.dumps(out), flush=True)
+    ctx.close()
 
 
 def pmc_traffic(config):
@@ -119,6 +220,10 @@ def main():
     spec = spec_from_file_location("knn_amd", os.path.join(REPO, "knn-using-p_threads-and-mpi_amd", "__init__.py"))
     knn = module_from_spec(spec)
     spec.loader.exec_module(knn)
+    if args.config == "L":
+        if world > 1:
+            raise SystemExit("config L is a single-GPU line (52.9 M pairs)")
+        return bench_arff(args, knn, torch, local)
 
     nt, nq_cfg, d, k, C, seed, scaling, dtype, sharding = CONFIGS[args.config]
     nt, nq_cfg = args.nt or nt, args.nq or nq_cfg
