@@ -54,6 +54,10 @@ MFMA_PEAK_TFLOPS = {  # MI355X_MICROARCH.md, dense
     "f32": 157.3,    # v_mfma_f32_32x32x2_f32
     "bf16": 2500.0,  # v_mfma_f32_32x32x16_bf16 (~2.5 PF dense)
 }
+# filter operand type (ctx.stats()["filter_operands"]) -> (peak of one algorithmic FLOP,
+# MFMA FLOP issued per algorithmic FLOP).  The split filter runs an fp32 dot as three bf16
+# MFMA products (hi.hi + hi.lo + lo.hi), so its roof is the bf16 dense peak / 3.
+FILTER_ROOF = {"f32": (157.3, 1), "bf16": (2500.0, 1), "bf16x3 split": (2500.0 / 3, 3)}
 
 
 def cpu_baseline(d, k, C, seed, kind=0):
@@ -192,7 +196,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="A", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--algo", default="auto", choices=["auto", "gemm", "direct"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "gemm", "gemm_split", "direct"])
     ap.add_argument("--splits", type=int, default=0, help="train segments per query tile (0 = auto)")
     ap.add_argument("--nt", type=int, default=0, help="override train rows (kernel studies)")
     ap.add_argument("--nq", type=int, default=0, help="override query rows (kernel studies)")
@@ -322,13 +326,20 @@ def main():
         filt_ms = stages.get("gemm_filter")
         roof = None
         if filt_ms:
-            peak = MFMA_PEAK_TFLOPS[dtype]
+            operands = stats.get("filter_operands") or dtype
+            peak, issued = FILTER_ROOF[operands]
             flops = 2.0 * d * nq * nt_local  # algorithmic: 2d FLOP per (query, train) pair, one launch
             ach = flops / (filt_ms * 1e-3) / 1e12
-            roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak,
+            roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1),
                     "unit": "TFLOP/s", "frac": round(ach / peak, 4),
-                    "traffic": pmc_traffic(args.config), "kernel": "k_gemm_filter",
+                    "traffic": pmc_traffic(args.config + ("" if operands == dtype else "/split")),
+                    "kernel": "k_gemm_filter", "filter_operands": operands,
                     "algorithmic_flops_per_launch": flops, "avg_launch_ms": round(filt_ms, 3)}
+            if issued > 1:
+                roof["peak_basis"] = (f"bf16 dense {MFMA_PEAK_TFLOPS['bf16']} TFLOP/s / {issued}: "
+                                      f"{issued} bf16 MFMA products per fp32 product (hi.hi + hi.lo + lo.hi)")
+                roof["mfma_flops_issued_per_launch"] = issued * flops
+                roof["x_fp32_mfma_peak"] = round(ach / MFMA_PEAK_TFLOPS["f32"], 3)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(d, k, C, seed, kind)

@@ -45,7 +45,11 @@ typedef enum { KNN_F32 = 0, KNN_BF16 = 1 } knn_dtype;
 typedef enum {
     KNN_ALGO_AUTO = 0,    /* direct form for low d / small problems, MFMA GEMM form otherwise */
     KNN_ALGO_DIRECT = 1,  /* fused direct-form distance + wave top-k + vote */
-    KNN_ALGO_GEMM = 2     /* ||q||^2+||t||^2-2q.t on MFMA (fp32 or bf16) + certified exact rescore */
+    KNN_ALGO_GEMM = 2,    /* ||q||^2+||t||^2-2q.t on MFMA (fp32 data: fp32 MFMA, bf16 data: bf16
+                             MFMA) + certified exact rescore */
+    KNN_ALGO_GEMM_SPLIT = 3 /* GEMM form with fp32 data split into bf16 hi + lo (q.t = hi.hi +
+                               hi.lo + lo.hi on the bf16 MFMA, fp32-grade certificate) + the
+                               same exact fp32 rescore; bf16 data: as KNN_ALGO_GEMM */
 } knn_algo;
 
 /* Context options.  One context drives one device (one HIP stream). */
@@ -134,7 +138,9 @@ knn_status knn_merge_vote_device(knn_ctx* ctx, int32_t nsrc, int64_t nq, int32_t
 int32_t knn_stage_times(const knn_ctx* ctx, const char** names, float* ms, int32_t n);
 
 /* Counters of the last predict call: [0] GEMM candidates kept, [1] queries sent to
- * the exact fallback, [2] train segments used.  Returns the number written. */
+ * the exact fallback, [2] train segments used, [3] filter operand type (-1 = no GEMM
+ * filter ran, 0 = fp32, 1 = bf16, 2 = bf16 hi/lo split of fp32).  Returns the number
+ * written. */
 int32_t knn_last_stats(const knn_ctx* ctx, int64_t* out, int32_t n);
 
 /*

@@ -59,6 +59,7 @@ struct knn_ctx {
     std::string err;
     // device workspace
     DBuf tnorm, tnp, qnorm, gthr, cnt, cand_idx, cand_L, cand_U, fb_list, ctrl, timing;
+    DBuf split_t, split_q;  // KNN_ALGO_GEMM_SPLIT: bf16 [hi | lo] copies of fp32 rows
     // host-API staging (device copies of host inputs / outputs)
     DBuf h_train, h_labels, h_test, h_pred, h_dist, h_idx;
     int32_t* ctrl_host = nullptr;  // pinned: [0] status, [1] fallback count
@@ -67,7 +68,7 @@ struct knn_ctx {
     std::vector<Stage> stages;
     std::vector<float> stage_ms;
     std::vector<const char*> stage_names;
-    int64_t stats[3] = {0, 0, 0};
+    int64_t stats[4] = {0, 0, 0, -1};  // candidates, fallback queries, segments, filter operand type
     int num_cus = 256;
 };
 
@@ -124,16 +125,29 @@ knn_status check_dataset(knn_ctx* c, const knn_dataset* x, const char* what, boo
     return KNN_OK;
 }
 
+// filter operand type of a GEMM-path call: fp32 data runs split (ELEM_SPLIT, bf16 hi/lo
+// rows of 4d bytes) under KNN_ALGO_GEMM_SPLIT, else the data's own type
+int filter_elem(int algo, int dtype) {
+    return (algo == KNN_ALGO_GEMM_SPLIT && dtype == KNN_F32) ? ELEM_SPLIT : dtype;
+}
+int filter_row_bytes(int felem, int d) { return felem == ELEM_SPLIT ? 4 * d : d * elem_size(felem); }
+
 int choose_algo(const knn_ctx* c, int64_t nt, int64_t nq, int d, int k, int dtype) {
     if (c->algo == KNN_ALGO_DIRECT) return KNN_ALGO_DIRECT;
     // the LDS-DMA filter stages whole rows: a row must be one of its tile widths
-    // (128, 256 or 512 bytes: fp32 d = 32/64/128, bf16 d = 64/128/256)
-    const int rb = d * elem_size(dtype);
-    bool gemm_ok = knn_gemm_filter_supported(dtype, rb) && k <= 128 && k <= nt &&
-                   knn_gemm_filter_lds(dtype, rb, k) <= 160 * 1024;
-    if (c->algo == KNN_ALGO_GEMM) return gemm_ok ? KNN_ALGO_GEMM : KNN_ALGO_DIRECT;
+    // (128, 256 or 512 bytes: fp32 d = 32/64/128 (fp32 or split), bf16 d = 64/128/256)
+    auto gemm_ok = [&](int algo) {
+        const int fe = filter_elem(algo, dtype), rb = filter_row_bytes(fe, d);
+        return knn_gemm_filter_supported(fe, rb) && k <= 128 && k <= nt &&
+               knn_gemm_filter_lds(fe, rb, k) <= 160 * 1024;
+    };
+    if (c->algo == KNN_ALGO_GEMM || c->algo == KNN_ALGO_GEMM_SPLIT)
+        return gemm_ok(c->algo) ? c->algo : KNN_ALGO_DIRECT;
     // AUTO: the direct form wins at low d (3 VALU ops per dim, no rescore) and on small jobs
-    if (gemm_ok && d >= 32 && nt >= 8192 && (double)nt * (double)nq >= 1e9) return KNN_ALGO_GEMM;
+    if (d >= 32 && nt >= 8192 && (double)nt * (double)nq >= 1e9) {
+        if (gemm_ok(KNN_ALGO_GEMM_SPLIT)) return KNN_ALGO_GEMM_SPLIT;
+        if (gemm_ok(KNN_ALGO_GEMM)) return KNN_ALGO_GEMM;
+    }
     return KNN_ALGO_DIRECT;
 }
 
@@ -174,8 +188,18 @@ knn_status run_direct(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, 
 //   fp32 MFMA (an exact fmaf chain):  coef = (4d+32) u, eta = (6d+8) 2^-149
 //   bf16 MFMA (products exact; internal sums assumed no worse than 2u per add, and
 //   denormal results possibly flushed):  coef = (6d+32) u, eta = (6d+8) 2^-125
-void certificate(int d, int dtype, float* coef, float* eta) {
-    if (dtype == KNN_BF16) {
+//   split (fp32 x = hi + lo + r, |r| <= 2^-16 |x| (+2^-134); q.t ~ hi.hi + hi.lo + lo.hi
+//   on the bf16 MFMA): the dropped terms lo.lo, (hi+lo) r_t, r_q (hi+lo) give
+//   <= 3.04 2^-16 sum|q_i t_i| <= 1.52 2^-16 N (N = qn + tn), i.e. <= 779 u N in G; the
+//   accumulation of 3d exact products at 2u per add gives <= 6.1 d u N in G; the norm
+//   and final-rounding terms are the fp32 ones, (3d+32) u N.  Flushed subnormal operands
+//   (<= 2^-126 |t_i| each, <= (1+N)/2 2^-126 by |t_i| <= (1+t_i^2)/2) add <= 3.1 d 2^-126
+//   (1+N).  coef = (10d + 840) u, eta = (8d+8) 2^-125.
+void certificate(int d, int felem, float* coef, float* eta) {
+    if (felem == ELEM_SPLIT) {
+        *coef = (float)(10 * d + 840) * 0x1p-24f;
+        *eta = (float)(8 * d + 8) * 0x1p-125f;
+    } else if (felem == KNN_BF16) {
         *coef = (float)(6 * d + 32) * 0x1p-24f;
         *eta = (float)(6 * d + 8) * 0x1p-125f;
     } else {
@@ -211,12 +235,13 @@ int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int
 }
 
 knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int k, int C,
-                    const QueryOut& out, hipStream_t st, bool* fell_back) {
+                    const QueryOut& out, hipStream_t st, int algo, bool* fell_back) {
     *fell_back = false;
     const int64_t nt = tr->n, nq = te->n;
     const int d = tr->d;
     const int dtype = tr->dtype;
-    const int rb = d * elem_size(dtype);
+    const int felem = filter_elem(algo, dtype);  // the filter's operand type
+    const int rb = filter_row_bytes(felem, d);
     const int cap = 64 * KNN_RESCORE_CAPW;
     HIP_OR_FAIL(c, c->tnorm.ensure(sizeof(float) * (nt + 64)));
     HIP_OR_FAIL(c, c->tnp.ensure(sizeof(float) * (nt + 64)));
@@ -229,7 +254,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     HIP_OR_FAIL(c, c->fb_list.ensure(sizeof(int32_t) * nq));
 
     float coef, eta;
-    certificate(d, dtype, &coef, &eta);
+    certificate(d, felem, &coef, &eta);
     stage_begin(c, st, "norms");
     HIP_OR_FAIL(c, knn_launch_row_norms(tr->feat, dtype, nt, tr->ld, d, c->tnorm.as<float>(),
                                         c->ctrl.as<int32_t>(), c->ctrl.as<uint32_t>() + 2,
@@ -253,14 +278,29 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     HIP_OR_FAIL(c, hipMemsetD32Async((hipDeviceptr_t)c->gthr.p, 0xFF800000u, nq, st));  // ordered(+inf)
     stage_end(c, st);
 
-    const FilterPlan plan = knn_gemm_filter_plan(dtype, rb, k);
+    // filter operands: the rows themselves, or their bf16 [hi | lo] split (2d elements per row)
+    const void* ftrain = tr->feat;
+    const void* ftest = te->feat;
+    int fld_t = tr->ld, fld_q = te->ld;
+    if (felem == ELEM_SPLIT) {
+        HIP_OR_FAIL(c, c->split_t.ensure(sizeof(uint16_t) * 2 * d * nt));
+        HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * 2 * d * nq));
+        stage_begin(c, st, "split");
+        HIP_OR_FAIL(c, knn_launch_split_rows((const float*)tr->feat, nt, tr->ld, d, c->split_t.as<uint16_t>(), st));
+        HIP_OR_FAIL(c, knn_launch_split_rows((const float*)te->feat, nq, te->ld, d, c->split_q.as<uint16_t>(), st));
+        stage_end(c, st);
+        ftrain = c->split_t.p; ftest = c->split_q.p;
+        fld_t = fld_q = 2 * d;
+    }
+
+    const FilterPlan plan = knn_gemm_filter_plan(felem, rb, k);
     const int64_t n_qtiles = (nq + plan.bm - 1) / plan.bm;
-    const int nseg = choose_splits(c, n_qtiles, nt, dtype, rb, k, cap);
+    const int nseg = choose_splits(c, n_qtiles, nt, felem, rb, k, cap);
     int64_t seg_len = (nt + nseg - 1) / nseg;
     seg_len = (seg_len + 63) / 64 * 64;
     GemmFilterArgs g{};
-    g.train = tr->feat; g.nt = nt; g.ld_t = tr->ld;
-    g.test = te->feat; g.nq = nq; g.ld_q = te->ld; g.d = d;
+    g.train = ftrain; g.nt = nt; g.ld_t = fld_t;
+    g.test = ftest; g.nq = nq; g.ld_q = fld_q; g.d = d;
     g.tnorm = c->tnorm.as<float>(); g.tnp = c->tnp.as<float>(); g.qnorm = c->qnorm.as<float>();
     g.tnmax = c->ctrl.as<uint32_t>() + 2;
     g.k = k; g.seg_len = seg_len; g.nseg = nseg; g.n_qtiles = (int)n_qtiles;
@@ -277,7 +317,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         g.timing = c->timing.as<unsigned long long>();
     }
     stage_begin(c, st, "gemm_filter");
-    HIP_OR_FAIL(c, knn_launch_gemm_filter(g, dtype, rb, st));
+    HIP_OR_FAIL(c, knn_launch_gemm_filter(g, felem, rb, st));
     stage_end(c, st);
     if (timing) {
         unsigned long long t[16];
@@ -304,6 +344,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     knn_status s = run_direct(c, tr, te, k, C, out, st, r.fb_list, r.fb_count);
     stage_end(c, st);
     c->stats[2] = nseg;
+    c->stats[3] = felem;
     return s;
 }
 
@@ -352,7 +393,7 @@ void knn_destroy(knn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (DBuf* b : {&c->tnorm, &c->tnp, &c->qnorm, &c->gthr, &c->cnt, &c->cand_idx, &c->cand_L, &c->cand_U,
-                    &c->fb_list, &c->ctrl, &c->timing, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
+                    &c->fb_list, &c->ctrl, &c->timing, &c->split_t, &c->split_q, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
                     &c->h_dist, &c->h_idx})
         b->release();
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
@@ -392,12 +433,14 @@ knn_status predict_core(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
     c->stages.clear();
     c->stats[0] = c->stats[1] = c->stats[2] = 0;
+    c->stats[3] = -1;
     if (te->n == 0) return KNN_OK;
     HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st));
     int algo = choose_algo(c, tr->n, te->n, tr->d, k, tr->dtype);
-    if (algo == KNN_ALGO_GEMM) {
+    const bool gemm = algo == KNN_ALGO_GEMM || algo == KNN_ALGO_GEMM_SPLIT;
+    if (gemm) {
         bool fb = false;
-        if ((s = run_gemm(c, tr, te, k, C, out, st, &fb)) != KNN_OK) return s;
+        if ((s = run_gemm(c, tr, te, k, C, out, st, algo, &fb)) != KNN_OK) return s;
     } else {
         stage_begin(c, st, "exact_scan");
         if ((s = run_direct(c, tr, te, k, C, out, st, nullptr, nullptr)) != KNN_OK) return s;
@@ -405,7 +448,7 @@ knn_status predict_core(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te
     }
     s = finish_call(c, st);
     c->stats[1] = c->ctrl_host[1];
-    if (c->profile >= 2 && algo == KNN_ALGO_GEMM) {
+    if (c->profile >= 2 && gemm) {
         // diagnostic only: total candidates kept by the filter
         std::vector<int32_t> h(te->n * 2 * c->stats[2]);
         if (hipMemcpy(h.data(), c->cnt.p, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost) == hipSuccess) {
@@ -522,7 +565,7 @@ int32_t knn_stage_times(const knn_ctx* c, const char** names, float* ms, int32_t
 
 int32_t knn_last_stats(const knn_ctx* c, int64_t* out, int32_t n) {
     if (!c || !out) return 0;
-    int32_t m = std::min(n, 3);
+    int32_t m = std::min(n, 4);
     for (int32_t i = 0; i < m; i++) out[i] = c->stats[i];
     return m;
 }

@@ -14,6 +14,9 @@
 // feature element types (knn_dtype): rows are fp32 or bf16 bits; every distance is the
 // reference's fp32 direct form on the (exactly) widened values
 enum { ELEM_F32 = 0, ELEM_BF16 = 1 };
+// filter-only operand type: fp32 rows split into bf16 [hi(d) | lo(d)] (k_split_rows), so
+// q.t ~ hi.hi + hi.lo + lo.hi runs on the bf16 MFMA with an fp32-grade error bound
+enum { ELEM_SPLIT = 2 };
 
 // Where a finished query's neighbours go.  pred may be NULL (train-shard mode: no vote);
 // dist/idx/label may be NULL; entry e of query q is at [q * stride + e]; idx is reported
@@ -81,6 +84,8 @@ FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k);
 hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st);
 size_t knn_gemm_filter_lds(int elem, int row_bytes, int k);
 hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks_per_cu);
+// fp32 rows [n][ld] (d % 4 == 0) -> bf16 rows [n][2d]: hi = rn(x), lo = rn(x - hi)
+hipError_t knn_launch_split_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st);
 hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st);
 hipError_t knn_launch_merge(const MergeArgs& a, hipStream_t st);
 hipError_t knn_launch_generate(const GenerateArgs& a, hipStream_t st);

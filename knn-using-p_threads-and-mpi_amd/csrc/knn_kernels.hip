@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <string>
+#include <type_traits>
 
 #include "knn_kernels.h"
 
@@ -122,6 +123,14 @@ __device__ __forceinline__ u64 list_at(const u64 (&T)[R], int e) {
 // ---------------------------------------------------------------------------------
 typedef uint16_t bf16_t;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+// filter operand tag for ELEM_SPLIT rows (bf16 bits [hi(d) | lo(d)] of fp32 data)
+struct split_t { uint16_t v; };
+
+// fp32 -> bf16 bits, round to nearest even (finite inputs)
+__device__ __forceinline__ uint32_t bf16_rne(float x) {
+    const uint32_t b = __float_as_uint(x);
+    return (b + 0x7fffu + ((b >> 16) & 1u)) >> 16;
+}
 
 __device__ __forceinline__ float widen(float v) { return v; }
 __device__ __forceinline__ float widen(bf16_t v) { return __uint_as_float((uint32_t)v << 16); }
@@ -333,9 +342,36 @@ __global__ __launch_bounds__(256) void k_row_norms(const E* __restrict__ x, int6
 }
 
 // ---------------------------------------------------------------------------------
+// k_split_rows: fp32 rows -> bf16 [hi | lo] rows for the split filter (ELEM_SPLIT).
+// hi = rn(x); x - hi is exact in fp32 (Sterbenz: hi is within 2^-8 |x| of x, or 0 when
+// |x| < 2^-134); lo = rn(x - hi).  |x - hi - lo| <= 2^-16 |x| + 2^-134.  One thread per
+// 4 elements (coalesced float4 in, two 8-byte bf16 quads out).
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_split_rows(const float* __restrict__ x, int64_t n, int ld, int d,
+                                                    bf16_t* __restrict__ out) {
+    const int per_row = d >> 2;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n * per_row) return;
+    const int64_t r = i / per_row;
+    const int c = (int)(i - r * per_row) * 4;
+    const float4 v = *reinterpret_cast<const float4*>(x + r * ld + c);
+    const float e[4] = {v.x, v.y, v.z, v.w};
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        hi[t] = bf16_rne(e[t]);
+        lo[t] = bf16_rne(e[t] - __uint_as_float(hi[t] << 16));
+    }
+    bf16_t* o = out + r * (int64_t)(2 * d) + c;
+    *reinterpret_cast<uint2*>(o) = make_uint2(hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16));
+    *reinterpret_cast<uint2*>(o + d) = make_uint2(lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16));
+}
+
+// ---------------------------------------------------------------------------------
 // k_gemm_filter<E, RB, MINB, NBUF, QG>: GEMM-form candidate filter on MFMA.
 //   E = float (RB/4-d rows, v_mfma_f32_32x32x2_f32, exact fp32) or bf16 (RB/2-d rows,
-//   v_mfma_f32_32x32x16_bf16); RB = bytes per row (128, 256, 512).
+//   v_mfma_f32_32x32x16_bf16) or split_t (fp32 data as RB/4-d [hi | lo] bf16 rows: three
+//   32x32x16 bf16 MFMAs per 16 features); RB = bytes per row (128, 256, 512).
 //
 // Block = 256 threads = 4 waves; each wave owns QG groups of 32 queries (BM = 128 QG
 // per block); a train tile holds BN = 32 RG rows with RG = 2 / QG, so every wave runs
@@ -456,6 +492,7 @@ template <typename E, int RB, int MINW, int NBUF, int NW, int QG, int RG>
 __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a) {
     typedef FilterTile<RB, NW, QG, RG> FT;
     constexpr bool BF = sizeof(E) == 2;
+    constexpr bool SPLIT = std::is_same<E, split_t>::value;  // [hi | lo] rows of fp32 data
     constexpr int NACC = FT::NACC, BN = FT::BN, BM = FT::BM, STRIDE = FT::STRIDE, SLOTS = FT::SLOTS;
     constexpr int DMA_INS = FT::DMA_INS, TILE = FT::TILE;
     constexpr int NT = 64 * NW;                    // threads per block
@@ -635,8 +672,20 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 #pragma unroll
                 for (int c = 0; c < NACC; c++) {
                     const bf16x8 A = __builtin_bit_cast(bf16x8, (RG == 2 && c) ? xb[s] : xa[s]);
-                    const bf16x8 B = __builtin_bit_cast(bf16x8, qf[qg_of(c)][s]);
-                    X[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B, X[c], 0, 0, 0);
+                    if constexpr (SPLIT) {
+                        // rows are [hi | lo]: steps s < NS/2 read t_hi (x q_hi, then x q_lo),
+                        // steps s >= NS/2 read t_lo (x q_hi); lo x lo is left out (certificate)
+                        constexpr int H2 = NS / 2;
+                        const int sq = s < H2 ? s : s - H2;
+                        X[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                            A, __builtin_bit_cast(bf16x8, qf[qg_of(c)][sq]), X[c], 0, 0, 0);
+                        if (s < H2)
+                            X[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                A, __builtin_bit_cast(bf16x8, qf[qg_of(c)][s + H2]), X[c], 0, 0, 0);
+                    } else {
+                        const bf16x8 B = __builtin_bit_cast(bf16x8, qf[qg_of(c)][s]);
+                        X[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B, X[c], 0, 0, 0);
+                    }
 #pragma unroll
                     for (int vv = 0; vv < VPS; vv++) {
 #ifndef KNN_ABLATE_NO_EPI
@@ -1320,11 +1369,11 @@ FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k) {
         FilterPlan f{nw, qg, rg, minw, nbuf, 32 * qg * nw, gemm_filter_lds_of(row_bytes, k, nw, qg, rg, nbuf)};
         return f;
     };
-    if (elem == ELEM_BF16 && (shape.empty() || shape == "w8")) {
+    if (elem != ELEM_F32 && (shape.empty() || shape == "w8")) {
         if (force_nb != 2 && fits(8, 1, 1, 3, cap)) return make(8, 1, 1, 2, 3);
         if (force_nb != 3 && fits(8, 1, 1, 2, cap)) return make(8, 1, 1, 2, 2);
     }
-    if (elem == ELEM_BF16 && shape == "w4q2") {
+    if (elem != ELEM_F32 && shape == "w4q2") {
         if (force_nb != 2 && fits(4, 2, 1, 3, cap)) return make(4, 2, 1, 1, 3);
         if (fits(4, 2, 1, 2, cap)) return make(4, 2, 1, 1, 2);
     }
@@ -1353,6 +1402,9 @@ static const void* gemm_filter_fn(const FilterPlan& f) {
 }
 
 static const void* gemm_filter_ptr(int elem, int row_bytes, const FilterPlan& f) {
+    if (elem == ELEM_SPLIT)
+        return row_bytes == 128 ? gemm_filter_fn<split_t, 128>(f)
+             : row_bytes == 256 ? gemm_filter_fn<split_t, 256>(f) : gemm_filter_fn<split_t, 512>(f);
     if (elem == ELEM_BF16)
         return row_bytes == 128 ? gemm_filter_fn<bf16_t, 128>(f)
              : row_bytes == 256 ? gemm_filter_fn<bf16_t, 256>(f) : gemm_filter_fn<bf16_t, 512>(f);
@@ -1433,6 +1485,15 @@ hipError_t knn_launch_confusion(const int32_t* pred, const int32_t* labels, int6
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
     hipLaunchKernelGGL(k_confusion, dim3(grid), dim3(256), 0, st, pred, labels, n, C, cm, correct, status);
+    KNN_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t knn_launch_split_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st) {
+    const int64_t total = n * (d / 4);
+    if (total <= 0) return hipSuccess;
+    if (d % 4 || ld % 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_split_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, n, ld, d, out);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -1,7 +1,9 @@
 """GPU parity: the HIP path through the C ABI vs the reference's fixtures and the oracle.
 
 Bar: bit-exact predictions, top-k train indices and top-k distance bits (the reference's
-direct-form fp32 distance, main.cpp:14-23), on both device algorithms.
+direct-form fp32 distance, main.cpp:14-23), on every device algorithm: the direct scan,
+the GEMM form on the fp32 MFMA and the GEMM form on the bf16 MFMA with fp32 rows split
+into bf16 hi + lo (gemm_split).
 """
 import os
 import subprocess
@@ -17,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def ctxs(knn):
-    out = {a: knn.Context(0, algo=a) for a in ("direct", "gemm", "auto")}
+    out = {a: knn.Context(0, algo=a) for a in ("direct", "gemm", "gemm_split", "auto")}
     yield out
     for c in out.values():
         c.close()
@@ -29,19 +31,24 @@ def arff(knn):
             for ds in DATASETS}
 
 
-@pytest.mark.parametrize("algo", ["direct", "gemm"])
+GEMM_OPERANDS = {"gemm": "f32", "gemm_split": "bf16x3 split"}
+
+
+@pytest.mark.parametrize("algo", ["direct", "gemm", "gemm_split"])
 @pytest.mark.parametrize("ds", DATASETS)
 @pytest.mark.parametrize("k", KS)
 def test_arff_golden(knn, ctxs, arff, algo, ds, k):
     (tf, tl, C), (qf, ql, Cq) = arff[ds]
-    if algo == "gemm":
+    if algo != "direct":
         # zero-pad d=7/11 to the filter's 32-wide tile: the extra (0-0)^2 terms add +0 at the
         # end of the sequential sum, so distances stay bit-identical to the reference
         tf = np.pad(tf, ((0, 0), (0, 32 - tf.shape[1])))
         qf = np.pad(qf, ((0, 0), (0, 32 - qf.shape[1])))
     pred, dist, idx = ctxs[algo].predict(tf, tl, qf, k, C, topk=True)
-    if algo == "gemm":
-        assert ctxs[algo].stats()["train_segments"] >= 1  # the MFMA filter path ran
+    if algo != "direct":
+        st = ctxs[algo].stats()
+        assert st["train_segments"] >= 1  # the MFMA filter path ran
+        assert st["filter_operands"] == GEMM_OPERANDS[algo]
     assert pred_sha(pred) == golden_manifest()[f"{ds}_k{k}"]["sha256"]
     gd, gi = golden_topk(ds, k)
     assert np.array_equal(idx, gi)
@@ -68,10 +75,11 @@ def test_synthetic_vs_oracle(knn, oracle, ctxs, d, k, nt, nq):
     te, _ = oracle.gen(7, 1, 0, nq, d)
     bad, opred, odist, oidx = oracle.knn(tr, tl, te, k, 10)
     assert bad == 0
-    for algo in ("direct", "gemm"):
+    for algo in ("direct", "gemm", "gemm_split"):
         pred, dist, idx = ctxs[algo].predict(tr, tl, te, k, 10, topk=True)
-        if algo == "gemm" and d in (32, 64, 128):
-            assert ctxs[algo].stats()["train_segments"] >= 1
+        if algo != "direct" and d in (32, 64, 128):
+            st = ctxs[algo].stats()
+            assert st["train_segments"] >= 1 and st["filter_operands"] == GEMM_OPERANDS[algo]
         assert np.array_equal(idx, oidx), algo
         assert np.array_equal(dist.view(np.uint32), odist.view(np.uint32)), algo
         assert np.array_equal(pred, opred), algo
@@ -86,9 +94,46 @@ def test_gemm_duplicates_and_ties(knn, oracle, ctxs):
     te = base[rng.integers(0, 50, size=100)] + 0.5 * rng.integers(0, 2, size=(100, 64)).astype(np.float32)
     for k in (1, 7, 64):
         bad, opred, odist, oidx = oracle.knn(tr, tl, te, k, 10)
-        pred, dist, idx = ctxs["gemm"].predict(tr, tl, te, k, 10, topk=True)
-        assert ctxs["gemm"].stats()["train_segments"] >= 1
-        assert np.array_equal(idx, oidx) and np.array_equal(pred, opred)
+        for algo in ("gemm", "gemm_split"):
+            pred, dist, idx = ctxs[algo].predict(tr, tl, te, k, 10, topk=True)
+            assert ctxs[algo].stats()["train_segments"] >= 1
+            assert np.array_equal(idx, oidx) and np.array_equal(pred, opred)
+
+
+@pytest.mark.parametrize("case", ["near_ties", "wide_range", "subnormal", "large"])
+def test_split_operands_stress(knn, oracle, ctxs, case):
+    """Inputs where a bf16 rounding of the rows alone would reorder neighbours: the split
+    filter's certificate (hi.hi + hi.lo + lo.hi) must still keep every true
+    neighbour, so results stay bit-identical to the reference's fp32 direct form."""
+    rng = np.random.default_rng({"near_ties": 11, "wide_range": 12, "subnormal": 13, "large": 14}[case])
+    nt, nq, d = 20000, 96, 64
+    if case == "near_ties":
+        # all rows within a few fp32 ulps of 1: every distance differs only below bf16 precision
+        base = np.ones((1, d), np.float32)
+        tr = base + rng.integers(-64, 65, size=(nt, d)).astype(np.float32) * np.float32(2.0 ** -23)
+        te = base + rng.integers(-64, 65, size=(nq, d)).astype(np.float32) * np.float32(2.0 ** -23)
+    elif case == "wide_range":
+        sc = np.float32(2.0) ** rng.integers(-40, 20, size=(1, d)).astype(np.float32)
+        tr = (rng.standard_normal((nt, d)).astype(np.float32) * sc).astype(np.float32)
+        te = (rng.standard_normal((nq, d)).astype(np.float32) * sc).astype(np.float32)
+    elif case == "subnormal":
+        tr = (rng.standard_normal((nt, d)) * 2.0 ** -135).astype(np.float32)
+        te = (rng.standard_normal((nq, d)) * 2.0 ** -135).astype(np.float32)
+        # half the columns normal (squares ~2^-120), half subnormal (2^-135)
+        tr[:, : d // 2] *= np.float32(2.0 ** 75)
+        te[:, : d // 2] *= np.float32(2.0 ** 75)
+    else:
+        tr = (rng.standard_normal((nt, d)) * 2.0 ** 55).astype(np.float32)
+        te = (rng.standard_normal((nq, d)) * 2.0 ** 55).astype(np.float32)
+    tl = rng.integers(0, 10, size=nt).astype(np.int32)
+    for k in (1, 10, 33):
+        bad, opred, odist, oidx = oracle.knn(tr, tl, te, k, 10)
+        if bad:
+            continue
+        pred, dist, idx = ctxs["gemm_split"].predict(tr, tl, te, k, 10, topk=True)
+        assert np.array_equal(idx, oidx), (case, k)
+        assert np.array_equal(dist.view(np.uint32), odist.view(np.uint32)), (case, k)
+        assert np.array_equal(pred, opred), (case, k)
 
 
 def test_edge_cases(knn, ctxs):
