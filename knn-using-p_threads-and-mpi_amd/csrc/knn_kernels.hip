@@ -938,8 +938,15 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
     // NBUF = 3 issues the next DMA after the slow path, so the slow path's stores are older
     // than it and the barrier's counted wait still leaves that DMA in flight (vmcnt retires in
     // issue order).  NBUF = 2 issues it inside the step: it must land by the next barrier.
-    constexpr bool LATE_DMA = NBUF == 3;
-    constexpr bool DEFER = NW == 8 && KNN_FILTER_DEFER;  // deferred slow path (see record())
+#ifndef KNN_FILTER_EARLY_DMA
+#define KNN_FILTER_EARLY_DMA 0  // NBUF = 3: issue the DMA inside the step as NBUF = 2 does
+#endif
+    // (early: a wave that stored after the DMA waits for everything at the next barrier)
+    constexpr bool LATE_DMA = NBUF == 3 && !KNN_FILTER_EARLY_DMA;
+#ifndef KNN_FILTER_DEFER_W4
+#define KNN_FILTER_DEFER_W4 0  // kernel studies: the deferred slow path in 4-wave blocks too
+#endif
+    constexpr bool DEFER = (NW == 8 || KNN_FILTER_DEFER_W4) && KNN_FILTER_DEFER;  // deferred slow path (see record())
     constexpr int DEFER_EVERY = 16;
     bool dirty = false;  // NBUF = 2: this wave issued vector-memory ops after the newest DMA
     auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
@@ -1351,11 +1358,12 @@ static size_t gemm_filter_lds_of(int row_bytes, int k, int nw, int qg, int rg, i
 //  fp32 (MFMA-bound, 16x the cycles per FLOP of bf16): 4 waves x 32 queries, 64-row tiles;
 //    two blocks per CU with double-buffered tiles when the LDS allows (one block's barrier /
 //    DMA phase hides under the other's MFMAs), else one block triple-buffered.
-//  bf16: 8 waves x 32 queries (two waves per SIMD hide each other's fast test, slow path and
-//    waits) over 32-row tiles: 256 queries share every staged train byte, so the L2 -> LDS
-//    bytes per FLOP halve; triple-buffered when the LDS allows.  Large k that does not fit
-//    falls back to the fp32 shape.
-// KNN_FILTER_NBUF=2|3 and KNN_FILTER_SHAPE=w8|w4q2|w4 (bf16) force a shape (kernel studies).
+//  bf16 / split: 8 waves x 32 queries (two waves per SIMD hide each other's fast test, slow
+//    path and waits): 256 queries share every staged train byte, so the L2 -> LDS bytes per
+//    FLOP halve.  64-row tiles (two accumulators per wave, double-buffered) when the LDS
+//    allows, else 32-row tiles, triple-buffered when the LDS allows (large k: big heaps).
+//    Larger k that does not fit falls back to the fp32 shape.
+// KNN_FILTER_NBUF=2|3 and KNN_FILTER_SHAPE=w8|w4r1|w4q2|w4 (bf16/split) force a shape (kernel studies).
 FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k) {
     const size_t cap = 160 * 1024;
     const char* env_nb = getenv("KNN_FILTER_NBUF");
@@ -1369,9 +1377,23 @@ FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k) {
         FilterPlan f{nw, qg, rg, minw, nbuf, 32 * qg * nw, gemm_filter_lds_of(row_bytes, k, nw, qg, rg, nbuf)};
         return f;
     };
+    if (elem != ELEM_F32 && (shape.empty() || shape == "w8r2")) {
+        // 8 waves x 32 queries over 64-row tiles (two accumulators per wave): half the
+        // barriers, waits and DMA-issue rounds per MFMA of the 32-row shape.  Double
+        // buffered: measured faster than triple on A and B (63 vs 69 ms, 1.42 vs 1.53 s)
+        if (force_nb != 3 && fits(8, 1, 2, 2, cap)) return make(8, 1, 2, 2, 2);
+        if (force_nb == 3 && fits(8, 1, 2, 3, cap)) return make(8, 1, 2, 2, 3);
+    }
     if (elem != ELEM_F32 && (shape.empty() || shape == "w8")) {
         if (force_nb != 2 && fits(8, 1, 1, 3, cap)) return make(8, 1, 1, 2, 3);
         if (force_nb != 3 && fits(8, 1, 1, 2, cap)) return make(8, 1, 1, 2, 2);
+    }
+    if (elem != ELEM_F32 && shape == "w4r1") {
+        // 4 waves x 32 queries over 32-row tiles, two blocks per CU: the two waves of a
+        // SIMD belong to different blocks, so one block's barrier / slow path runs under
+        // the other's MFMAs (at twice the L2 -> LDS bytes per FLOP of the 8-wave block)
+        if (force_nb != 2 && fits(4, 1, 1, 3, cap / 2)) return make(4, 1, 1, 2, 3);
+        if (fits(4, 1, 1, 2, cap / 2)) return make(4, 1, 1, 2, 2);
     }
     if (elem != ELEM_F32 && shape == "w4q2") {
         if (force_nb != 2 && fits(4, 2, 1, 3, cap)) return make(4, 2, 1, 1, 3);
@@ -1393,7 +1415,9 @@ template <typename E, int RB>
 static const void* gemm_filter_fn(const FilterPlan& f) {
 #define KNN_FILTER_FN(MINW, NBUF, NW, QG, RG) reinterpret_cast<const void*>(&k_gemm_filter<E, RB, MINW, NBUF, NW, QG, RG>)
     if constexpr (sizeof(E) == 2) {
+        if (f.nw == 8 && f.rg == 2) return f.nbuf == 3 ? KNN_FILTER_FN(2, 3, 8, 1, 2) : KNN_FILTER_FN(2, 2, 8, 1, 2);
         if (f.nw == 8) return f.nbuf == 3 ? KNN_FILTER_FN(2, 3, 8, 1, 1) : KNN_FILTER_FN(2, 2, 8, 1, 1);
+        if (f.rg == 1 && f.qg == 1) return f.nbuf == 3 ? KNN_FILTER_FN(2, 3, 4, 1, 1) : KNN_FILTER_FN(2, 2, 4, 1, 1);
         if (f.qg == 2) return f.nbuf == 3 ? KNN_FILTER_FN(1, 3, 4, 2, 1) : KNN_FILTER_FN(1, 2, 4, 2, 1);
     }
     if (f.minw == 2) return KNN_FILTER_FN(2, 2, 4, 1, 2);
