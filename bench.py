@@ -57,7 +57,10 @@ MFMA_PEAK_TFLOPS = {  # MI355X_MICROARCH.md, dense
 # filter operand type (ctx.stats()["filter_operands"]) -> (peak of one algorithmic FLOP,
 # MFMA FLOP issued per algorithmic FLOP).  The split filter runs an fp32 dot as three bf16
 # MFMA products (hi.hi + hi.lo + lo.hi), so its roof is the bf16 dense peak / 3.
-FILTER_ROOF = {"f32": (157.3, 1), "bf16": (2500.0, 1), "bf16x3 split": (2500.0 / 3, 3)}
+FILTER_ROOF = {"f32": (157.3, 1), "bf16": (2500.0, 1), "bf16x3 split": (2500.0 / 3, 3),
+               "bf16 rounded": (2500.0, 1)}
+# pmc summary key suffix per filter operand type on fp32 data
+PMC_SUFFIX = {"bf16x3 split": "/split", "bf16 rounded": "/bf16r"}
 
 
 def cpu_baseline(d, k, C, seed, kind=0):
@@ -196,7 +199,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="A", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--algo", default="auto", choices=["auto", "gemm", "gemm_split", "direct"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "gemm", "gemm_split", "gemm_bf16", "direct"])
     ap.add_argument("--splits", type=int, default=0, help="train segments per query tile (0 = auto)")
     ap.add_argument("--nt", type=int, default=0, help="override train rows (kernel studies)")
     ap.add_argument("--nq", type=int, default=0, help="override query rows (kernel studies)")
@@ -332,7 +335,7 @@ def main():
             ach = flops / (filt_ms * 1e-3) / 1e12
             roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1),
                     "unit": "TFLOP/s", "frac": round(ach / peak, 4),
-                    "traffic": pmc_traffic(args.config + ("" if operands == dtype else "/split")),
+                    "traffic": pmc_traffic(args.config + ("" if operands == dtype else PMC_SUFFIX.get(operands, "/" + operands))),
                     "kernel": "k_gemm_filter", "filter_operands": operands,
                     "algorithmic_flops_per_launch": flops, "avg_launch_ms": round(filt_ms, 3)}
             if issued > 1:

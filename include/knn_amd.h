@@ -47,9 +47,15 @@ typedef enum {
     KNN_ALGO_DIRECT = 1,  /* fused direct-form distance + wave top-k + vote */
     KNN_ALGO_GEMM = 2,    /* ||q||^2+||t||^2-2q.t on MFMA (fp32 data: fp32 MFMA, bf16 data: bf16
                              MFMA) + certified exact rescore */
-    KNN_ALGO_GEMM_SPLIT = 3 /* GEMM form with fp32 data split into bf16 hi + lo (q.t = hi.hi +
+    KNN_ALGO_GEMM_SPLIT = 3, /* GEMM form with fp32 data split into bf16 hi + lo (q.t = hi.hi +
                                hi.lo + lo.hi on the bf16 MFMA, fp32-grade certificate) + the
                                same exact fp32 rescore; bf16 data: as KNN_ALGO_GEMM */
+    KNN_ALGO_GEMM_BF16 = 4  /* GEMM form with fp32 data rounded to bf16 for the filter only (one
+                               bf16 MFMA per 16 features, certificate widened by the rounding
+                               error, 2^-7 (|q|^2+|t|^2)) + the same exact fp32 rescore; AUTO
+                               runs it first and re-runs a call as KNN_ALGO_GEMM_SPLIT when
+                               more than 1/16 of its queries overflow their candidate lists.
+                               bf16 data: as KNN_ALGO_GEMM */
 } knn_algo;
 
 /* Context options.  One context drives one device (one HIP stream). */
@@ -139,7 +145,8 @@ int32_t knn_stage_times(const knn_ctx* ctx, const char** names, float* ms, int32
 
 /* Counters of the last predict call: [0] GEMM candidates kept, [1] queries sent to
  * the exact fallback, [2] train segments used, [3] filter operand type (-1 = no GEMM
- * filter ran, 0 = fp32, 1 = bf16, 2 = bf16 hi/lo split of fp32).  Returns the number
+ * filter ran, 0 = fp32, 1 = bf16, 2 = bf16 hi/lo split of fp32, 3 = bf16 rounding of
+ * fp32), [4] 1 when AUTO re-ran the call with the split filter.  Returns the number
  * written. */
 int32_t knn_last_stats(const knn_ctx* ctx, int64_t* out, int32_t n);
 

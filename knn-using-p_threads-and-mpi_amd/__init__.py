@@ -32,8 +32,8 @@ KNN_OK, KNN_EINVAL, KNN_ENOMEM, KNN_EHIP, KNN_ERANGE, KNN_ENODEV, KNN_EIO = rang
 STATUS_NAMES = {0: "KNN_OK", 1: "KNN_EINVAL", 2: "KNN_ENOMEM", 3: "KNN_EHIP", 4: "KNN_ERANGE",
                 5: "KNN_ENODEV", 6: "KNN_EIO"}
 KNN_F32, KNN_BF16 = 0, 1
-ALGOS = {"auto": 0, "direct": 1, "gemm": 2, "gemm_split": 3}
-FILTER_OPERANDS = {-1: None, 0: "f32", 1: "bf16", 2: "bf16x3 split"}
+ALGOS = {"auto": 0, "direct": 1, "gemm": 2, "gemm_split": 3, "gemm_bf16": 4}
+FILTER_OPERANDS = {-1: None, 0: "f32", 1: "bf16", 2: "bf16x3 split", 3: "bf16 rounded"}
 
 
 class KnnError(RuntimeError):
@@ -335,10 +335,10 @@ class Context:
         return out
 
     def stats(self):
-        v = (ctypes.c_int64 * 4)()
-        self.lib.knn_last_stats(self.h, v, 4)
+        v = (ctypes.c_int64 * 5)()
+        self.lib.knn_last_stats(self.h, v, 5)
         return {"candidates": v[0], "fallback_queries": v[1], "train_segments": v[2],
-                "filter_operands": FILTER_OPERANDS.get(v[3], v[3])}
+                "filter_operands": FILTER_OPERANDS.get(v[3], v[3]), "rerun_split": bool(v[4])}
 
 
 _default_ctx = None

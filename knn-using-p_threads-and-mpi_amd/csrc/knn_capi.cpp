@@ -59,7 +59,7 @@ struct knn_ctx {
     std::string err;
     // device workspace
     DBuf tnorm, tnp, qnorm, gthr, cnt, cand_idx, cand_L, cand_U, fb_list, ctrl, timing;
-    DBuf split_t, split_q;  // KNN_ALGO_GEMM_SPLIT: bf16 [hi | lo] copies of fp32 rows
+    DBuf split_t, split_q;  // KNN_ALGO_GEMM_SPLIT / _BF16: bf16 [hi | lo] / rn copies of fp32 rows
     // host-API staging (device copies of host inputs / outputs)
     DBuf h_train, h_labels, h_test, h_pred, h_dist, h_idx;
     int32_t* ctrl_host = nullptr;  // pinned: [0] status, [1] fallback count
@@ -68,7 +68,7 @@ struct knn_ctx {
     std::vector<Stage> stages;
     std::vector<float> stage_ms;
     std::vector<const char*> stage_names;
-    int64_t stats[4] = {0, 0, 0, -1};  // candidates, fallback queries, segments, filter operand type
+    int64_t stats[5] = {0, 0, 0, -1, 0};  // candidates, fallback queries, segments, filter operand type, rerun
     int num_cus = 256;
 };
 
@@ -126,11 +126,18 @@ knn_status check_dataset(knn_ctx* c, const knn_dataset* x, const char* what, boo
 }
 
 // filter operand type of a GEMM-path call: fp32 data runs split (ELEM_SPLIT, bf16 hi/lo
-// rows of 4d bytes) under KNN_ALGO_GEMM_SPLIT, else the data's own type
+// rows of 4d bytes) under KNN_ALGO_GEMM_SPLIT, rounded (ELEM_ROUND, bf16 rows of 2d bytes)
+// under KNN_ALGO_GEMM_BF16, else the data's own type
 int filter_elem(int algo, int dtype) {
-    return (algo == KNN_ALGO_GEMM_SPLIT && dtype == KNN_F32) ? ELEM_SPLIT : dtype;
+    if (dtype != KNN_F32) return dtype;
+    return algo == KNN_ALGO_GEMM_SPLIT ? ELEM_SPLIT : algo == KNN_ALGO_GEMM_BF16 ? ELEM_ROUND : dtype;
 }
-int filter_row_bytes(int felem, int d) { return felem == ELEM_SPLIT ? 4 * d : d * elem_size(felem); }
+int filter_row_bytes(int felem, int d) {
+    return felem == ELEM_SPLIT ? 4 * d : felem == ELEM_ROUND ? 2 * d : d * elem_size(felem);
+}
+bool is_gemm(int algo) {
+    return algo == KNN_ALGO_GEMM || algo == KNN_ALGO_GEMM_SPLIT || algo == KNN_ALGO_GEMM_BF16;
+}
 
 int choose_algo(const knn_ctx* c, int64_t nt, int64_t nq, int d, int k, int dtype) {
     if (c->algo == KNN_ALGO_DIRECT) return KNN_ALGO_DIRECT;
@@ -141,10 +148,13 @@ int choose_algo(const knn_ctx* c, int64_t nt, int64_t nq, int d, int k, int dtyp
         return knn_gemm_filter_supported(fe, rb) && k <= 128 && k <= nt &&
                knn_gemm_filter_lds(fe, rb, k) <= 160 * 1024;
     };
-    if (c->algo == KNN_ALGO_GEMM || c->algo == KNN_ALGO_GEMM_SPLIT)
+    if (is_gemm(c->algo))
         return gemm_ok(c->algo) ? c->algo : KNN_ALGO_DIRECT;
-    // AUTO: the direct form wins at low d (3 VALU ops per dim, no rescore) and on small jobs
+    // AUTO: the direct form wins at low d (3 VALU ops per dim, no rescore) and on small jobs;
+    // above that the rounded bf16 filter (one MFMA per 16 features), re-run as split when
+    // its wider certificate overflows the candidate lists (predict_core)
     if (d >= 32 && nt >= 8192 && (double)nt * (double)nq >= 1e9) {
+        if (gemm_ok(KNN_ALGO_GEMM_BF16)) return KNN_ALGO_GEMM_BF16;
         if (gemm_ok(KNN_ALGO_GEMM_SPLIT)) return KNN_ALGO_GEMM_SPLIT;
         if (gemm_ok(KNN_ALGO_GEMM)) return KNN_ALGO_GEMM;
     }
@@ -195,8 +205,16 @@ knn_status run_direct(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, 
 //   and final-rounding terms are the fp32 ones, (3d+32) u N.  Flushed subnormal operands
 //   (<= 2^-126 |t_i| each, <= (1+N)/2 2^-126 by |t_i| <= (1+t_i^2)/2) add <= 3.1 d 2^-126
 //   (1+N).  coef = (10d + 840) u, eta = (8d+8) 2^-125.
+//   rounded (fp32 x -> bf16 rn(x), |rn(x) - x| <= 2^-8 |x| (+2^-134)): each product moves by
+//   <= (2^-7 + 2^-16) |q_i t_i|, in sum <= (2^-7 + 2^-16) N/2, i.e. <= 131328 u N in G; the
+//   accumulation of d exact products at 2u per add gives <= 2.02 d u N in G; norm and final
+//   roundings (3d+32) u N; L/U/Delta roundings and slack within 512 u N.  Flushed or
+//   subnormal operands as for split.  coef = (6d + 131840) u, eta = (8d+8) 2^-125.
 void certificate(int d, int felem, float* coef, float* eta) {
-    if (felem == ELEM_SPLIT) {
+    if (felem == ELEM_ROUND) {
+        *coef = (float)(6 * d + 131840) * 0x1p-24f;
+        *eta = (float)(8 * d + 8) * 0x1p-125f;
+    } else if (felem == ELEM_SPLIT) {
         *coef = (float)(10 * d + 840) * 0x1p-24f;
         *eta = (float)(8 * d + 8) * 0x1p-125f;
     } else if (felem == KNN_BF16) {
@@ -235,13 +253,14 @@ int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int
 }
 
 knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int k, int C,
-                    const QueryOut& out, hipStream_t st, int algo, bool* fell_back) {
+                    const QueryOut& out, hipStream_t st, int algo, bool* fell_back, int64_t retry_limit = -1) {
     *fell_back = false;
     const int64_t nt = tr->n, nq = te->n;
     const int d = tr->d;
     const int dtype = tr->dtype;
     const int felem = filter_elem(algo, dtype);  // the filter's operand type
     const int rb = filter_row_bytes(felem, d);
+    const int kelem = felem == ELEM_ROUND ? ELEM_BF16 : felem;  // ELEM_ROUND runs the bf16 kernel
     const int cap = 64 * KNN_RESCORE_CAPW;
     HIP_OR_FAIL(c, c->tnorm.ensure(sizeof(float) * (nt + 64)));
     HIP_OR_FAIL(c, c->tnp.ensure(sizeof(float) * (nt + 64)));
@@ -291,11 +310,20 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         stage_end(c, st);
         ftrain = c->split_t.p; ftest = c->split_q.p;
         fld_t = fld_q = 2 * d;
+    } else if (felem == ELEM_ROUND) {
+        HIP_OR_FAIL(c, c->split_t.ensure(sizeof(uint16_t) * d * nt));
+        HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * d * nq));
+        stage_begin(c, st, "round");
+        HIP_OR_FAIL(c, knn_launch_round_rows((const float*)tr->feat, nt, tr->ld, d, c->split_t.as<uint16_t>(), st));
+        HIP_OR_FAIL(c, knn_launch_round_rows((const float*)te->feat, nq, te->ld, d, c->split_q.as<uint16_t>(), st));
+        stage_end(c, st);
+        ftrain = c->split_t.p; ftest = c->split_q.p;
+        fld_t = fld_q = d;
     }
 
-    const FilterPlan plan = knn_gemm_filter_plan(felem, rb, k);
+    const FilterPlan plan = knn_gemm_filter_plan(kelem, rb, k);
     const int64_t n_qtiles = (nq + plan.bm - 1) / plan.bm;
-    const int nseg = choose_splits(c, n_qtiles, nt, felem, rb, k, cap);
+    const int nseg = choose_splits(c, n_qtiles, nt, kelem, rb, k, cap);
     int64_t seg_len = (nt + nseg - 1) / nseg;
     seg_len = (seg_len + 63) / 64 * 64;
     GemmFilterArgs g{};
@@ -317,7 +345,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         g.timing = c->timing.as<unsigned long long>();
     }
     stage_begin(c, st, "gemm_filter");
-    HIP_OR_FAIL(c, knn_launch_gemm_filter(g, felem, rb, st));
+    HIP_OR_FAIL(c, knn_launch_gemm_filter(g, kelem, rb, st));
     stage_end(c, st);
     if (timing) {
         unsigned long long t[16];
@@ -340,11 +368,20 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     HIP_OR_FAIL(c, knn_launch_rescore(r, st));
     stage_end(c, st);
 
+    c->stats[2] = nseg;
+    c->stats[3] = felem;
+    if (retry_limit >= 0) {
+        // AUTO's rounded filter: too many overflowing queries -> the caller re-runs as split
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->ctrl_host, c->ctrl.p, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        HIP_OR_FAIL(c, hipStreamSynchronize(st));
+        if (c->ctrl_host[1] > retry_limit) {
+            *fell_back = true;
+            return KNN_OK;
+        }
+    }
     stage_begin(c, st, "fallback_scan");
     knn_status s = run_direct(c, tr, te, k, C, out, st, r.fb_list, r.fb_count);
     stage_end(c, st);
-    c->stats[2] = nseg;
-    c->stats[3] = felem;
     return s;
 }
 
@@ -432,15 +469,25 @@ knn_status predict_core(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te
     HIP_OR_FAIL(c, hipSetDevice(c->device));
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
     c->stages.clear();
-    c->stats[0] = c->stats[1] = c->stats[2] = 0;
+    c->stats[0] = c->stats[1] = c->stats[2] = c->stats[4] = 0;
     c->stats[3] = -1;
     if (te->n == 0) return KNN_OK;
     HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st));
     int algo = choose_algo(c, tr->n, te->n, tr->d, k, tr->dtype);
-    const bool gemm = algo == KNN_ALGO_GEMM || algo == KNN_ALGO_GEMM_SPLIT;
+    const bool gemm = is_gemm(algo);
     if (gemm) {
         bool fb = false;
-        if ((s = run_gemm(c, tr, te, k, C, out, st, algo, &fb)) != KNN_OK) return s;
+        // AUTO on fp32 data runs the rounded filter first; when more than 1/16 of the queries
+        // (at least 256) overflow its candidate lists, the call is re-run with the split
+        // filter (every output is rewritten; the fallback scan of the first run is skipped)
+        const bool adaptive = c->algo == KNN_ALGO_AUTO && filter_elem(algo, tr->dtype) == ELEM_ROUND;
+        const int64_t limit = adaptive ? std::max<int64_t>(256, te->n / 16) : -1;
+        if ((s = run_gemm(c, tr, te, k, C, out, st, algo, &fb, limit)) != KNN_OK) return s;
+        if (adaptive && fb && !(c->ctrl_host[0] & KNN_STATUS_GEMM_UNSAFE)) {
+            HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.as<int32_t>() + 1, 0, sizeof(int32_t), st));
+            c->stats[4] = 1;
+            if ((s = run_gemm(c, tr, te, k, C, out, st, KNN_ALGO_GEMM_SPLIT, &fb)) != KNN_OK) return s;
+        }
     } else {
         stage_begin(c, st, "exact_scan");
         if ((s = run_direct(c, tr, te, k, C, out, st, nullptr, nullptr)) != KNN_OK) return s;
@@ -565,7 +612,7 @@ int32_t knn_stage_times(const knn_ctx* c, const char** names, float* ms, int32_t
 
 int32_t knn_last_stats(const knn_ctx* c, int64_t* out, int32_t n) {
     if (!c || !out) return 0;
-    int32_t m = std::min(n, 4);
+    int32_t m = std::min(n, 5);
     for (int32_t i = 0; i < m; i++) out[i] = c->stats[i];
     return m;
 }

@@ -17,6 +17,9 @@ enum { ELEM_F32 = 0, ELEM_BF16 = 1 };
 // filter-only operand type: fp32 rows split into bf16 [hi(d) | lo(d)] (k_split_rows), so
 // q.t ~ hi.hi + hi.lo + lo.hi runs on the bf16 MFMA with an fp32-grade error bound
 enum { ELEM_SPLIT = 2 };
+// filter-only operand type: fp32 rows rounded to bf16 (k_round_rows, d elements per row);
+// the filter runs the bf16 kernel on them under a certificate widened by the rounding
+enum { ELEM_ROUND = 3 };
 
 // Where a finished query's neighbours go.  pred may be NULL (train-shard mode: no vote);
 // dist/idx/label may be NULL; entry e of query q is at [q * stride + e]; idx is reported
@@ -86,6 +89,7 @@ size_t knn_gemm_filter_lds(int elem, int row_bytes, int k);
 hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks_per_cu);
 // fp32 rows [n][ld] (d % 4 == 0) -> bf16 rows [n][2d]: hi = rn(x), lo = rn(x - hi)
 hipError_t knn_launch_split_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st);
+hipError_t knn_launch_round_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st);
 hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st);
 hipError_t knn_launch_merge(const MergeArgs& a, hipStream_t st);
 hipError_t knn_launch_generate(const GenerateArgs& a, hipStream_t st);

@@ -368,6 +368,24 @@ __global__ __launch_bounds__(256) void k_split_rows(const float* __restrict__ x,
 }
 
 // ---------------------------------------------------------------------------------
+// k_round_rows: fp32 rows -> bf16 rows rn(x) for the rounded filter (ELEM_ROUND, d
+// elements per row): |x - rn(x)| <= 2^-8 |x| + 2^-134.  The filter runs the bf16 kernel
+// on them; the certificate (knn_capi.cpp) carries the rounding.  One thread per 4
+// elements (coalesced float4 in, one 8-byte bf16 quad out).
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_round_rows(const float* __restrict__ x, int64_t n, int ld, int d,
+                                                    bf16_t* __restrict__ out) {
+    const int per_row = d >> 2;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n * per_row) return;
+    const int64_t r = i / per_row;
+    const int c = (int)(i - r * per_row) * 4;
+    const float4 v = *reinterpret_cast<const float4*>(x + r * ld + c);
+    *reinterpret_cast<uint2*>(out + r * (int64_t)d + c) =
+        make_uint2(bf16_rne(v.x) | (bf16_rne(v.y) << 16), bf16_rne(v.z) | (bf16_rne(v.w) << 16));
+}
+
+// ---------------------------------------------------------------------------------
 // k_gemm_filter<E, RB, MINB, NBUF, QG>: GEMM-form candidate filter on MFMA.
 //   E = float (RB/4-d rows, v_mfma_f32_32x32x2_f32, exact fp32) or bf16 (RB/2-d rows,
 //   v_mfma_f32_32x32x16_bf16) or split_t (fp32 data as RB/4-d [hi | lo] bf16 rows: three
@@ -1429,7 +1447,7 @@ static const void* gemm_filter_ptr(int elem, int row_bytes, const FilterPlan& f)
     if (elem == ELEM_SPLIT)
         return row_bytes == 128 ? gemm_filter_fn<split_t, 128>(f)
              : row_bytes == 256 ? gemm_filter_fn<split_t, 256>(f) : gemm_filter_fn<split_t, 512>(f);
-    if (elem == ELEM_BF16)
+    if (elem == ELEM_BF16 || elem == ELEM_ROUND)
         return row_bytes == 128 ? gemm_filter_fn<bf16_t, 128>(f)
              : row_bytes == 256 ? gemm_filter_fn<bf16_t, 256>(f) : gemm_filter_fn<bf16_t, 512>(f);
     return row_bytes == 128 ? gemm_filter_fn<float, 128>(f)
@@ -1518,6 +1536,15 @@ hipError_t knn_launch_split_rows(const float* x, int64_t n, int ld, int d, uint1
     if (total <= 0) return hipSuccess;
     if (d % 4 || ld % 4) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_split_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, n, ld, d, out);
+    KNN_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t knn_launch_round_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st) {
+    const int64_t total = n * (d / 4);
+    if (total <= 0) return hipSuccess;
+    if (d % 4 || ld % 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_round_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, n, ld, d, out);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }

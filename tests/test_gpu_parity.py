@@ -3,7 +3,9 @@
 Bar: bit-exact predictions, top-k train indices and top-k distance bits (the reference's
 direct-form fp32 distance, main.cpp:14-23), on every device algorithm: the direct scan,
 the GEMM form on the fp32 MFMA and the GEMM form on the bf16 MFMA with fp32 rows split
-into bf16 hi + lo (gemm_split).
+into bf16 hi + lo (gemm_split), and the GEMM form on the bf16 MFMA with fp32 rows rounded
+to bf16 for the filter only (gemm_bf16; AUTO re-runs it as split when its candidate lists
+overflow).
 """
 import os
 import subprocess
@@ -19,7 +21,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def ctxs(knn):
-    out = {a: knn.Context(0, algo=a) for a in ("direct", "gemm", "gemm_split", "auto")}
+    out = {a: knn.Context(0, algo=a) for a in ("direct", "gemm", "gemm_split", "gemm_bf16", "auto")}
     yield out
     for c in out.values():
         c.close()
@@ -31,10 +33,12 @@ def arff(knn):
             for ds in DATASETS}
 
 
-GEMM_OPERANDS = {"gemm": "f32", "gemm_split": "bf16x3 split"}
+GEMM_OPERANDS = {"gemm": "f32", "gemm_split": "bf16x3 split", "gemm_bf16": "bf16 rounded"}
+# feature counts whose filter rows are one of the LDS-DMA tile widths (128/256/512 B)
+GEMM_DIMS = {"gemm": (32, 64, 128), "gemm_split": (32, 64, 128), "gemm_bf16": (64, 128, 256)}
 
 
-@pytest.mark.parametrize("algo", ["direct", "gemm", "gemm_split"])
+@pytest.mark.parametrize("algo", ["direct", "gemm", "gemm_split", "gemm_bf16"])
 @pytest.mark.parametrize("ds", DATASETS)
 @pytest.mark.parametrize("k", KS)
 def test_arff_golden(knn, ctxs, arff, algo, ds, k):
@@ -42,8 +46,9 @@ def test_arff_golden(knn, ctxs, arff, algo, ds, k):
     if algo != "direct":
         # zero-pad d=7/11 to the filter's 32-wide tile: the extra (0-0)^2 terms add +0 at the
         # end of the sequential sum, so distances stay bit-identical to the reference
-        tf = np.pad(tf, ((0, 0), (0, 32 - tf.shape[1])))
-        qf = np.pad(qf, ((0, 0), (0, 32 - qf.shape[1])))
+        w = GEMM_DIMS[algo][0]
+        tf = np.pad(tf, ((0, 0), (0, w - tf.shape[1])))
+        qf = np.pad(qf, ((0, 0), (0, w - qf.shape[1])))
     pred, dist, idx = ctxs[algo].predict(tf, tl, qf, k, C, topk=True)
     if algo != "direct":
         st = ctxs[algo].stats()
@@ -75,9 +80,9 @@ def test_synthetic_vs_oracle(knn, oracle, ctxs, d, k, nt, nq):
     te, _ = oracle.gen(7, 1, 0, nq, d)
     bad, opred, odist, oidx = oracle.knn(tr, tl, te, k, 10)
     assert bad == 0
-    for algo in ("direct", "gemm", "gemm_split"):
+    for algo in ("direct", "gemm", "gemm_split", "gemm_bf16"):
         pred, dist, idx = ctxs[algo].predict(tr, tl, te, k, 10, topk=True)
-        if algo != "direct" and d in (32, 64, 128):
+        if algo != "direct" and d in GEMM_DIMS[algo]:
             st = ctxs[algo].stats()
             assert st["train_segments"] >= 1 and st["filter_operands"] == GEMM_OPERANDS[algo]
         assert np.array_equal(idx, oidx), algo
@@ -94,14 +99,15 @@ def test_gemm_duplicates_and_ties(knn, oracle, ctxs):
     te = base[rng.integers(0, 50, size=100)] + 0.5 * rng.integers(0, 2, size=(100, 64)).astype(np.float32)
     for k in (1, 7, 64):
         bad, opred, odist, oidx = oracle.knn(tr, tl, te, k, 10)
-        for algo in ("gemm", "gemm_split"):
+        for algo in ("gemm", "gemm_split", "gemm_bf16"):
             pred, dist, idx = ctxs[algo].predict(tr, tl, te, k, 10, topk=True)
             assert ctxs[algo].stats()["train_segments"] >= 1
             assert np.array_equal(idx, oidx) and np.array_equal(pred, opred)
 
 
+@pytest.mark.parametrize("algo", ["gemm_split", "gemm_bf16"])
 @pytest.mark.parametrize("case", ["near_ties", "wide_range", "subnormal", "large"])
-def test_split_operands_stress(knn, oracle, ctxs, case):
+def test_split_operands_stress(knn, oracle, ctxs, case, algo):
     """Inputs where a bf16 rounding of the rows alone would reorder neighbours: the split
     filter's certificate (hi.hi + hi.lo + lo.hi) must still keep every true
     neighbour, so results stay bit-identical to the reference's fp32 direct form."""
@@ -130,10 +136,38 @@ def test_split_operands_stress(knn, oracle, ctxs, case):
         bad, opred, odist, oidx = oracle.knn(tr, tl, te, k, 10)
         if bad:
             continue
-        pred, dist, idx = ctxs["gemm_split"].predict(tr, tl, te, k, 10, topk=True)
+        pred, dist, idx = ctxs[algo].predict(tr, tl, te, k, 10, topk=True)
+        assert ctxs[algo].stats()["filter_operands"] == GEMM_OPERANDS[algo]
         assert np.array_equal(idx, oidx), (case, k)
         assert np.array_equal(dist.view(np.uint32), odist.view(np.uint32)), (case, k)
         assert np.array_equal(pred, opred), (case, k)
+
+
+@pytest.mark.parametrize("case", ["near_ties", "uniform"])
+def test_auto_rounded_filter_rerun(knn, oracle, ctxs, case):
+    """AUTO on fp32 data runs the rounded bf16 filter; when its wider certificate overflows
+    more than 1/16 of the candidate lists (rows within a few ulps of 1: every row passes)
+    the call is re-run with the split filter.  Either way the results are the exact
+    direct-form scan's (GPU direct path, itself checked against the oracle above)."""
+    rng = np.random.default_rng(21)
+    nt, nq, d = 160000, 6400, 64  # nt * nq >= 1e9: AUTO takes the GEMM path
+    if case == "near_ties":
+        tr = 1 + rng.integers(-64, 65, size=(nt, d)).astype(np.float32) * np.float32(2.0 ** -23)
+        te = 1 + rng.integers(-64, 65, size=(nq, d)).astype(np.float32) * np.float32(2.0 ** -23)
+        tr, te = tr.astype(np.float32), te.astype(np.float32)
+        tl = rng.integers(0, 10, size=nt).astype(np.int32)
+    else:
+        tr, tl = oracle.gen(9, 0, 0, nt, d)
+        te, _ = oracle.gen(9, 1, 0, nq, d)
+    k = 10
+    pred, dist, idx = ctxs["auto"].predict(tr, tl, te, k, 10, topk=True)
+    st = ctxs["auto"].stats()
+    assert st["rerun_split"] == (case == "near_ties"), st
+    assert st["filter_operands"] == ("bf16x3 split" if case == "near_ties" else "bf16 rounded"), st
+    dpred, ddist, didx = ctxs["direct"].predict(tr, tl, te, k, 10, topk=True)
+    assert np.array_equal(idx, didx)
+    assert np.array_equal(dist.view(np.uint32), ddist.view(np.uint32))
+    assert np.array_equal(pred, dpred)
 
 
 def test_edge_cases(knn, ctxs):
