@@ -38,6 +38,10 @@
 typedef unsigned long long u64;
 static constexpr u64 KEY_NONE = ~0ull;
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+#ifndef KNN_FILTER_PK
+#define KNN_FILTER_PK 0
+#endif
 
 // ---------------------------------------------------------------------------------
 // Keys and wave-level bitonic networks (64 lanes, one element per lane per register)
@@ -670,6 +674,20 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
                 t4[ta] = *reinterpret_cast<const float4*>(tnpY + 32 * ta + 8 * (reg >> 2) + 4 * h);
             return fmaf(-2.0f, Y[acc][reg], f4get(t4[ta], reg & 3));
         };
+#if KNN_FILTER_PK
+        // study variant: two adjacent fast-test values (v even) in one v_pk_fma_f32 (the same
+        // correctly rounded fma per element), folded into the running minimum by v_min3_f32
+        auto epi_y2 = [&](int v, float& m) __attribute__((always_inline)) {
+            const int acc = v >> 4, reg = v & 15, ta = rg_of(acc);
+            if ((reg & 3) == 0 && (RG == 2 || acc == 0))
+                t4[ta] = *reinterpret_cast<const float4*>(tnpY + 32 * ta + 8 * (reg >> 2) + 4 * h);
+            const floatx2 tt = (reg & 2) ? floatx2{t4[ta].z, t4[ta].w} : floatx2{t4[ta].x, t4[ta].y};
+            const floatx2 yy = floatx2{Y[acc][reg], Y[acc][reg + 1]};
+            floatx2 y;
+            asm volatile("v_pk_fma_f32 %0, %1, -2.0, %2 op_sel_hi:[1,0,1]" : "=v"(y) : "v"(yy), "v"(tt));
+            asm volatile("v_min3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(m), "v"(y.x), "v"(y.y));
+        };
+#endif
         if constexpr (BF) {
             // one 32x32x16 MFMA per 16-B fragment: prefetch the A fragments PF k-steps ahead
             // and interleave the previous tile's fast test between the MFMAs
@@ -707,6 +725,12 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 #pragma unroll
                     for (int vv = 0; vv < VPS; vv++) {
 #ifndef KNN_ABLATE_NO_EPI
+#if KNN_FILTER_PK
+                        if constexpr (VPS % 2 == 0) {
+                            if (vv % 2 == 0) epi_y2(16 * c + s * VPS + vv, mn[c]);
+                            continue;
+                        }
+#endif
                         const float y = epi_y(16 * c + s * VPS + vv);
                         asm volatile("" ::"v"(y));  // computed here, beside this MFMA
                         mn[c] = fminf(mn[c], y);
@@ -1381,7 +1405,8 @@ static size_t gemm_filter_lds_of(int row_bytes, int k, int nw, int qg, int rg, i
 //    FLOP halve.  64-row tiles (two accumulators per wave, double-buffered) when the LDS
 //    allows, else 32-row tiles, triple-buffered when the LDS allows (large k: big heaps).
 //    Larger k that does not fit falls back to the fp32 shape.
-// KNN_FILTER_NBUF=2|3 and KNN_FILTER_SHAPE=w8|w4r1|w4q2|w4 (bf16/split) force a shape (kernel studies).
+//  bf16 rows of 128 bytes (64 features): 4 waves x 32 queries, 64-row tiles, two blocks per CU.
+// KNN_FILTER_NBUF=2|3 and KNN_FILTER_SHAPE=w8r2|w8|w4r1|w4q2|w4 (bf16/split) force a shape (kernel studies).
 FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k) {
     const size_t cap = 160 * 1024;
     const char* env_nb = getenv("KNN_FILTER_NBUF");
@@ -1395,6 +1420,13 @@ FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k) {
         FilterPlan f{nw, qg, rg, minw, nbuf, 32 * qg * nw, gemm_filter_lds_of(row_bytes, k, nw, qg, rg, nbuf)};
         return f;
     };
+    if (elem != ELEM_F32 && shape.empty() && row_bytes == 128 && fits(4, 1, 2, 2, cap / 2)) {
+        // short rows (64 bf16 features: 4 MFMAs per 32x32 block and tile): the per-tile
+        // barrier and fast test outweigh the MFMAs, so two 4-wave blocks per CU hide each
+        // other's synchronisation.  Measured on B (rounded bf16, k=32): 880 ms vs 1062 ms
+        // for w8r2 on the same box; on A (128 features) w8r2 stays ahead (37.0 vs 40.7 ms)
+        return make(4, 1, 2, 2, 2);
+    }
     if (elem != ELEM_F32 && (shape.empty() || shape == "w8r2")) {
         // 8 waves x 32 queries over 64-row tiles (two accumulators per wave): half the
         // barriers, waits and DMA-issue rounds per MFMA of the 32-row shape.  Double
