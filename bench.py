@@ -305,6 +305,7 @@ def main():
         ctx = knn.Context(local, algo=args.algo, train_splits=args.splits, profile=2)
         step()
         cand = ctx.stats()["candidates"]
+        stats["candidates"] = cand  # the timed steps do not count them (profile=2 pass only)
         esz = 2 if dtype == "bf16" else 4
         nseg = max(1, stats["train_segments"])
         resc_ms = stage_sum["rescore"] / args.steps

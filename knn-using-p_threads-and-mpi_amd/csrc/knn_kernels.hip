@@ -428,7 +428,7 @@ __global__ __launch_bounds__(256) void k_round_rows(const float* __restrict__ x,
 // ---------------------------------------------------------------------------------
 static constexpr int GF_BM1 = 128;  // queries per block per query group
 #ifndef KNN_FILTER_DEFER
-#define KNN_FILTER_DEFER 1  // 8-wave shape: record passing values, flush them every 16 tiles
+#define KNN_FILTER_DEFER 1  // 8-wave shape: record passing values, flush them every KNN_FILTER_DEFER_EVERY tiles
 #endif
 #ifndef KNN_FILTER_PF
 #define KNN_FILTER_PF 6  // A-fragment prefetch depth in MFMAs (bf16)
@@ -923,7 +923,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
     // tile (one wave's heap work then no longer holds the other seven at each barrier),
     // or at once when some lane's queue is full.  A threshold that waits for the flush is
     // stale but still valid (it only ever tightens).
-    constexpr int RQ = 4;
+#ifndef KNN_FILTER_RQ
+#define KNN_FILTER_RQ 4  // deferred-queue depth per lane
+#endif
+    constexpr int RQ = KNN_FILTER_RQ;
     float qL[RQ], qU[RQ];
     int qT[RQ];
     bool qG[RQ];
@@ -989,7 +992,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 #define KNN_FILTER_DEFER_W4 0  // kernel studies: the deferred slow path in 4-wave blocks too
 #endif
     constexpr bool DEFER = (NW == 8 || KNN_FILTER_DEFER_W4) && KNN_FILTER_DEFER;  // deferred slow path (see record())
-    constexpr int DEFER_EVERY = 16;
+#ifndef KNN_FILTER_DEFER_EVERY
+#define KNN_FILTER_DEFER_EVERY 64  // tiles between flushes of the deferred queues (16: A 37.1 ms, 32: 36.4, 64: 35.8)
+#endif
+    constexpr int DEFER_EVERY = KNN_FILTER_DEFER_EVERY;
     bool dirty = false;  // NBUF = 2: this wave issued vector-memory ops after the newest DMA
     auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
         const int64_t r0 = row_begin + (int64_t)it * BN;

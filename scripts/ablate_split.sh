@@ -3,7 +3,7 @@
 # prints the per-phase clocks of the timing builds
 set -o pipefail
 mkdir -p gpurun_out
-B="python -u bench.py --config ${CFG:-A} --algo gemm_split --steps 2 --warmup 1 --no-cpu-baseline"
+B="python -u bench.py --config ${CFG:-A} --algo ${ALGO:-gemm_split} --steps 2 --warmup 1 --no-cpu-baseline"
 for v in ${VARIANTS:-base noslow noepi nodma timing tnoslow}; do
   if [ $v = base ]; then L=""; else L="KNN_AMD_LIB=$PWD/knn-using-p_threads-and-mpi_amd/build/ablate/libknn_amd_$v.so"; fi
   case $v in t*) L="$L KNN_FILTER_TIMING=1";; esac
