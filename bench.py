@@ -344,6 +344,11 @@ def main():
                                       f"{issued} bf16 MFMA products per fp32 product (hi.hi + hi.lo + lo.hi)")
                 roof["mfma_flops_issued_per_launch"] = issued * flops
                 roof["x_fp32_mfma_peak"] = round(ach / MFMA_PEAK_TFLOPS["f32"], 3)
+            elif operands == "bf16 rounded":
+                roof["peak_basis"] = (f"bf16 dense {MFMA_PEAK_TFLOPS['bf16']} TFLOP/s: fp32 rows rounded to bf16 "
+                                      "for the filter only (one bf16 MFMA product per fp32 product); "
+                                      "distances re-scored exactly in fp32")
+                roof["x_fp32_mfma_peak"] = round(ach / MFMA_PEAK_TFLOPS["f32"], 3)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(d, k, C, seed, kind)
