@@ -91,6 +91,16 @@ hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks
 hipError_t knn_launch_split_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st);
 hipError_t knn_launch_round_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st);
 hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st);
+// Starting thresholds of the GEMM filter (k_seed_threshold): gthr[q] = ordered k-th
+// smallest exact D from query q to ns <= KNN_SEED_MAX_ROWS rows spread over train.
+#define KNN_SEED_MAX_ROWS 2048
+struct SeedArgs {
+    const void* train; int64_t nt; int ld_t;
+    const void* test; int64_t nq; int ld_q; int d; int k;
+    int ns; int ld_lds;
+    uint32_t* gthr;
+};
+hipError_t knn_launch_seed_threshold(const SeedArgs& a, int elem, hipStream_t st);
 hipError_t knn_launch_merge(const MergeArgs& a, hipStream_t st);
 hipError_t knn_launch_generate(const GenerateArgs& a, hipStream_t st);
 hipError_t knn_launch_confusion(const int32_t* pred, const int32_t* labels, int64_t n, int C, int32_t* cm,

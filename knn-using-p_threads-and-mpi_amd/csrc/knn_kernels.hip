@@ -1540,6 +1540,69 @@ hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st) {
     return a.elem == ELEM_BF16 ? launch_rescore_e<bf16_t>(a, st) : launch_rescore_e<float>(a, st);
 }
 
+// ---------------------------------------------------------------------------------
+// k_seed_threshold<E>: a valid starting threshold for the GEMM filter.  One wave per
+// query computes the exact direct-form D (direct_dist, as the rescore does) to ns rows
+// spread evenly over the train set and stores the k-th smallest as ordered bits in gthr.
+// Any k real rows have a k-th distance >= D_(k), the true k-th distance, so every row of
+// the exact top-k still has L <= D <= D_(k) <= thr and is kept: the filter only starts
+// its scan from this bound instead of +inf (no heap-filling phase of all-passing tiles).
+// A D that is not < FLT_MAX never counts; with fewer than k finite D, gthr stays +inf.
+// LDS per wave: the query row widened to fp32 [ld_lds].
+// ---------------------------------------------------------------------------------
+constexpr int SEED_PER_LANE = KNN_SEED_MAX_ROWS / 64;
+template <typename E>
+__global__ __launch_bounds__(256) void k_seed_threshold(SeedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = lane_id();
+    const int wave = threadIdx.x >> 6;
+    float* qs = reinterpret_cast<float*>(smem) + (size_t)wave * a.ld_lds;
+    const int64_t q = (int64_t)blockIdx.x * 4 + wave;
+    if (q >= a.nq) return;
+    const E* train = reinterpret_cast<const E*>(a.train);
+    const E* test = reinterpret_cast<const E*>(a.test);
+    for (int i = lane; i < a.d; i += 64) qs[i] = widen(test[q * a.ld_q + i]);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    uint32_t o[SEED_PER_LANE];
+    int valid = 0;
+#pragma unroll
+    for (int i = 0; i < SEED_PER_LANE; i++) {
+        const int sidx = lane + 64 * i;
+        uint32_t v = 0xffffffffu;
+        if (sidx < a.ns) {
+            const int64_t t = (int64_t)sidx * a.nt / a.ns;  // distinct rows: ns <= nt
+            const float D = direct_dist(qs, train + t * a.ld_t, a.d);
+            if (D < FLT_MAX) v = f2o(D);
+        }
+        o[i] = v;
+        valid += __popcll(__ballot(v != 0xffffffffu));
+    }
+    if (valid < a.k) return;
+    // smallest x with #{o <= x} >= k
+    uint32_t lo = 0u, hi = 0xfffffffeu;
+    while (lo < hi) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        int c = 0;
+#pragma unroll
+        for (int i = 0; i < SEED_PER_LANE; i++) c += __popcll(__ballot(o[i] <= mid));
+        if (c >= a.k) hi = mid; else lo = mid + 1;
+    }
+    if (lane == 0) a.gthr[q] = lo;
+}
+
+hipError_t knn_launch_seed_threshold(const SeedArgs& a, int elem, hipStream_t st) {
+    if (a.nq <= 0 || a.ns < a.k || a.ns > a.nt || a.ns > KNN_SEED_MAX_ROWS || a.ld_lds < a.d) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)((a.nq + 3) / 4);
+    const size_t lds = 4 * (size_t)a.ld_lds * sizeof(float);
+    if (elem == ELEM_BF16)
+        hipLaunchKernelGGL(k_seed_threshold<bf16_t>, dim3(grid), dim3(256), lds, st, a);
+    else
+        hipLaunchKernelGGL(k_seed_threshold<float>, dim3(grid), dim3(256), lds, st, a);
+    KNN_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 template <int R>
 static hipError_t launch_merge_r(const MergeArgs& a, hipStream_t st) {
     const unsigned grid = (unsigned)((a.nq + 3) / 4);
