@@ -44,18 +44,21 @@ typedef enum { KNN_F32 = 0, KNN_BF16 = 1 } knn_dtype;
 
 typedef enum {
     KNN_ALGO_AUTO = 0,    /* direct form for low d / small problems, MFMA GEMM form otherwise */
-    KNN_ALGO_DIRECT = 1,  /* fused direct-form distance + wave top-k + vote */
+    KNN_ALGO_DIRECT = 1,  /* direct form, tiled (k_direct_tile: LDS-staged train tiles shared by
+                             the queries of a block, scalar query operands, wave top-k + vote) */
     KNN_ALGO_GEMM = 2,    /* ||q||^2+||t||^2-2q.t on MFMA (fp32 data: fp32 MFMA, bf16 data: bf16
                              MFMA) + certified exact rescore */
     KNN_ALGO_GEMM_SPLIT = 3, /* GEMM form with fp32 data split into bf16 hi + lo (q.t = hi.hi +
                                hi.lo + lo.hi on the bf16 MFMA, fp32-grade certificate) + the
                                same exact fp32 rescore; bf16 data: as KNN_ALGO_GEMM */
-    KNN_ALGO_GEMM_BF16 = 4  /* GEMM form with fp32 data rounded to bf16 for the filter only (one
+    KNN_ALGO_GEMM_BF16 = 4, /* GEMM form with fp32 data rounded to bf16 for the filter only (one
                                bf16 MFMA per 16 features, certificate widened by the rounding
                                error, 2^-7 (|q|^2+|t|^2)) + the same exact fp32 rescore; AUTO
                                runs it first and re-runs a call as KNN_ALGO_GEMM_SPLIT when
                                more than 1/16 of its queries overflow their candidate lists.
                                bf16 data: as KNN_ALGO_GEMM */
+    KNN_ALGO_DIRECT_SCAN = 5 /* direct form, one block per query (k_exact_scan, the GEMM path's
+                                per-query fallback) */
 } knn_algo;
 
 /* Context options.  One context drives one device (one HIP stream). */

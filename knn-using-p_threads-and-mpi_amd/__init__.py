@@ -32,7 +32,7 @@ KNN_OK, KNN_EINVAL, KNN_ENOMEM, KNN_EHIP, KNN_ERANGE, KNN_ENODEV, KNN_EIO = rang
 STATUS_NAMES = {0: "KNN_OK", 1: "KNN_EINVAL", 2: "KNN_ENOMEM", 3: "KNN_EHIP", 4: "KNN_ERANGE",
                 5: "KNN_ENODEV", 6: "KNN_EIO"}
 KNN_F32, KNN_BF16 = 0, 1
-ALGOS = {"auto": 0, "direct": 1, "gemm": 2, "gemm_split": 3, "gemm_bf16": 4}
+ALGOS = {"auto": 0, "direct": 1, "gemm": 2, "gemm_split": 3, "gemm_bf16": 4, "direct_scan": 5}
 FILTER_OPERANDS = {-1: None, 0: "f32", 1: "bf16", 2: "bf16x3 split", 3: "bf16 rounded"}
 
 
@@ -141,10 +141,46 @@ def _tensor_dtype(t):
     raise KnnError(KNN_EINVAL, f"features must be float32 or bfloat16, got {t.dtype}")
 
 
+def _check_tensor(t, name, dtype, n=None):
+    """A device output/label tensor: contiguous, of the element type the C ABI reads."""
+    import torch
+    if t.dtype != dtype:
+        raise KnnError(KNN_EINVAL, f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise KnnError(KNN_EINVAL, f"{name} must be contiguous")
+    if n is not None and t.numel() < n:
+        raise KnnError(KNN_EINVAL, f"{name} holds {t.numel()} elements, needs {n}")
+    return t
+
+
 def _device_dataset(feat, labels=None, d=None):
+    """A [n][ld] device tensor (unit stride along features; ld = its row stride) and its
+    int32 labels -> knn_dataset.  Views such as x[:, :64] of a wider tensor are accepted
+    (ld = the parent's row stride); anything with non-unit feature stride is rejected."""
+    import torch
+    if feat.dim() != 2:
+        raise KnnError(KNN_EINVAL, "features must be a 2-D [n][ld] tensor")
+    if feat.shape[0] > 1 and feat.stride(1) != 1:
+        raise KnnError(KNN_EINVAL, "features must have unit stride along the feature axis")
+    ld = feat.stride(0) if feat.shape[0] > 1 else feat.shape[1]
     d = feat.shape[1] if d is None else d
+    if d > feat.shape[1]:
+        raise KnnError(KNN_EINVAL, f"d={d} exceeds the tensor's {feat.shape[1]} columns")
+    if labels is not None:
+        _check_tensor(labels, "labels", torch.int32, feat.shape[0])
     return knn_dataset(feat.data_ptr(), None if labels is None else labels.data_ptr(), feat.shape[0], d,
-                       feat.shape[1], _tensor_dtype(feat))
+                       ld, _tensor_dtype(feat))
+
+
+def _outputs(nq, k, pred=None, dist=None, idx=None):
+    """Type/shape checks of device outputs (pred int32 [nq], dist float32 / idx int32 [nq][k])."""
+    import torch
+    if pred is not None:
+        _check_tensor(pred, "pred", torch.int32, nq)
+    if dist is not None:
+        _check_tensor(dist, "dist", torch.float32, nq * k)
+    if idx is not None:
+        _check_tensor(idx, "idx", torch.int32, nq * k)
 
 
 def shard_range(n, world, rank):
@@ -275,6 +311,7 @@ class Context:
         train/test: [n][ld] float32 contiguous; labels/pred/idx int32; dist float32."""
         tr = _device_dataset(train, labels, d)
         te = _device_dataset(test, None, d)
+        _outputs(te.n, k, pred, dist, idx)
         self._check(self.lib.knn_predict_device(
             self.h, ctypes.byref(tr), ctypes.byref(te), k, num_classes, pred.data_ptr(),
             None if dist is None else dist.data_ptr(), None if idx is None else idx.data_ptr(),
@@ -287,6 +324,8 @@ class Context:
         te = _device_dataset(test, None, d)
         if tuple(rec.shape) != (test.shape[0], 3, k):
             raise KnnError(KNN_EINVAL, f"rec must be [{test.shape[0]}, 3, {k}]")
+        import torch
+        _check_tensor(rec, "rec", torch.int32)
         self._check(self.lib.knn_shard_topk_device(
             self.h, ctypes.byref(tr), ctypes.byref(te), k, num_classes, idx_base, rec.data_ptr(),
             None if stream is None else ctypes.c_void_p(stream)))
@@ -296,6 +335,9 @@ class Context:
         nsrc, nq = rec.shape[0], rec.shape[1]
         if tuple(rec.shape[2:]) != (3, k) or pred.shape[0] != nq:
             raise KnnError(KNN_EINVAL, "rec must be [nsrc][nq][3][k] and pred [nq]")
+        import torch
+        _check_tensor(rec, "rec", torch.int32)
+        _outputs(nq, k, pred, dist, idx)
         self._check(self.lib.knn_merge_vote_device(
             self.h, nsrc, nq, k, num_classes, rec.data_ptr(), pred.data_ptr(),
             None if dist is None else dist.data_ptr(), None if idx is None else idx.data_ptr(),
@@ -315,6 +357,8 @@ class Context:
         """computeConfusionMatrix / computeAccuracy (main.cpp:87-112) on device tensors:
         returns (cm int32 [C][C] device tensor, accuracy as the reference's float)."""
         import torch
+        _check_tensor(pred, "pred", torch.int32)
+        _check_tensor(labels, "labels", torch.int32, pred.shape[0])
         if cm is None:
             cm = torch.empty((num_classes, num_classes), dtype=torch.int32, device=pred.device)
         corr = torch.zeros(1, dtype=torch.int64, device=pred.device)

@@ -60,6 +60,10 @@ struct knn_ctx {
     // device workspace
     DBuf tnorm, tnp, qnorm, gthr, cnt, cand_idx, cand_L, cand_U, fb_list, ctrl, timing;
     DBuf split_t, split_q;  // KNN_ALGO_GEMM_SPLIT / _BF16: bf16 [hi | lo] / rn copies of fp32 rows
+    DBuf seg_rec;           // k_direct_tile segment records [nseg][nq][3][k]
+    // kernel-study switches, read once from the environment in knn_create (never in a call)
+    int study_seed = 0, study_timing = 0;
+    FilterStudy fstudy{0, {0}};
     // host-API staging (device copies of host inputs / outputs)
     DBuf h_train, h_labels, h_test, h_pred, h_dist, h_idx;
     int32_t* ctrl_host = nullptr;  // pinned: [0] status, [1] fallback count
@@ -140,13 +144,13 @@ bool is_gemm(int algo) {
 }
 
 int choose_algo(const knn_ctx* c, int64_t nt, int64_t nq, int d, int k, int dtype) {
-    if (c->algo == KNN_ALGO_DIRECT) return KNN_ALGO_DIRECT;
+    if (c->algo == KNN_ALGO_DIRECT || c->algo == KNN_ALGO_DIRECT_SCAN) return c->algo;
     // the LDS-DMA filter stages whole rows: a row must be one of its tile widths
     // (128, 256 or 512 bytes: fp32 d = 32/64/128 (fp32 or split), bf16 d = 64/128/256)
     auto gemm_ok = [&](int algo) {
         const int fe = filter_elem(algo, dtype), rb = filter_row_bytes(fe, d);
         return knn_gemm_filter_supported(fe, rb) && k <= 128 && k <= nt &&
-               knn_gemm_filter_lds(fe, rb, k) <= 160 * 1024;
+               knn_gemm_filter_lds(fe, rb, k, &c->fstudy) <= 160 * 1024;
     };
     if (is_gemm(c->algo))
         return gemm_ok(c->algo) ? c->algo : KNN_ALGO_DIRECT;
@@ -180,15 +184,66 @@ knn_status finish_call(knn_ctx* c, hipStream_t st) {
     return KNN_OK;
 }
 
-knn_status run_direct(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int k, int C,
-                      const QueryOut& out, hipStream_t st, const int32_t* qlist, const int32_t* qcount) {
+// k_direct_tile segments: enough (query block, segment) units to fill whole waves of
+// resident blocks (more segments only when they raise the filled fraction by > 2 %, each
+// one costs a merge pass), at least 4 tiles per segment, records within 2 GB
+int choose_direct_segments(const knn_ctx* c, int64_t nt, int64_t nq, int d, int k, int C, int elem) {
+    const int qb = knn_direct_tile_qb(k);
+    const int64_t nqb = (nq + qb - 1) / qb;
+    int occ = 1;
+    if (knn_direct_tile_occupancy(k, elem, d, C, &occ) != hipSuccess || occ < 1) occ = 1;
+    const int64_t slots = (int64_t)occ * c->num_cus;
+    int best = 1;
+    double best_eff = 0.0;
+    for (int s = 1; s <= 32; s++) {
+        if (s > 1 && nt / s < 256) break;
+        if (s > 1 && (double)s * (double)nq * 12.0 * k > 2e9) break;
+        const int64_t w = nqb * s;
+        const double eff = (double)w / (double)(((w + slots - 1) / slots) * slots);
+        if (eff > best_eff + 0.02) { best = s; best_eff = eff; }
+    }
+    return best;
+}
+
+// the direct form over the whole query set: k_direct_tile (+ k_merge_vote of its segments)
+knn_status run_direct_tile(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int k, int C,
+                           const QueryOut& out, hipStream_t st) {
+    DirectTileArgs a{};
+    a.train = tr->feat; a.labels = tr->labels; a.nt = tr->n; a.ld_t = tr->ld;
+    a.test = te->feat; a.ld_q = te->ld; a.nq = te->n;
+    a.d = tr->d; a.k = k; a.C = C; a.elem = tr->dtype;
+    a.status = c->ctrl.as<int32_t>();
+    const int nseg = c->train_splits > 0 ? std::min(32, c->train_splits)
+                                         : choose_direct_segments(c, tr->n, te->n, tr->d, k, C, tr->dtype);
+    a.nseg = nseg;
+    a.seg_len = (tr->n + nseg - 1) / nseg;
+    c->stats[2] = nseg;
+    if (nseg == 1) {
+        a.out = out;
+        HIP_OR_FAIL(c, knn_launch_direct_tile(a, st));
+        return KNN_OK;
+    }
+    HIP_OR_FAIL(c, c->seg_rec.ensure(sizeof(int32_t) * 3 * (size_t)k * (size_t)te->n * nseg));
+    a.rec = c->seg_rec.as<int32_t>();
+    HIP_OR_FAIL(c, knn_launch_direct_tile(a, st));
+    MergeArgs m{};
+    m.rec = a.rec; m.nsrc = nseg; m.nq = te->n; m.k = k; m.C = C;
+    m.out = out; m.status = a.status; m.labels = tr->labels;
+    HIP_OR_FAIL(c, knn_launch_merge(m, st));
+    return KNN_OK;
+}
+
+// one k_exact_scan block per query: KNN_ALGO_DIRECT_SCAN over every query, or the GEMM
+// path's fallback over a device-side query list (qlist / qcount)
+knn_status run_exact_scan(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int k, int C,
+                          const QueryOut& out, hipStream_t st, const int32_t* qlist, const int32_t* qcount) {
     ExactScanArgs a{};
     a.train = tr->feat; a.labels = tr->labels; a.nt = tr->n; a.ld_t = tr->ld;
     a.test = te->feat; a.ld_q = te->ld; a.nq = te->n;
     a.d = tr->d; a.k = k; a.C = C; a.elem = tr->dtype;
     a.qlist = qlist; a.qcount = qcount;
     a.out = out; a.status = c->ctrl.as<int32_t>();
-    int grid = qlist ? std::max(1, 2 * c->num_cus) : (int)std::min<int64_t>(te->n, 16384);
+    const int grid = qlist ? std::max(1, 2 * c->num_cus) : (int)std::min<int64_t>(te->n, 16384);
     if (grid <= 0) return KNN_OK;
     HIP_OR_FAIL(c, knn_launch_exact_scan(a, grid, st));
     return KNN_OK;
@@ -235,7 +290,7 @@ int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int
     // tile; the slice gets a 1.5x margin.  Overflowing queries still finish exactly,
     // on the slow full-scan fallback.
     int occ = 1;
-    if (knn_gemm_filter_occupancy(dtype, rb, k, &occ) != hipSuccess || occ < 1) occ = 1;
+    if (knn_gemm_filter_occupancy(dtype, rb, k, &occ, &c->fstudy) != hipSuccess || occ < 1) occ = 1;
     const int64_t slots = (int64_t)occ * c->num_cus;
     int best = 1;
     double best_eff = 0.0;
@@ -287,8 +342,8 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     if (c->ctrl_host[0] & KNN_STATUS_GEMM_UNSAFE) {
         HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st));
         *fell_back = true;
-        stage_begin(c, st, "exact_scan");
-        knn_status s = run_direct(c, tr, te, k, C, out, st, nullptr, nullptr);
+        stage_begin(c, st, "direct_tile");
+        knn_status s = run_direct_tile(c, tr, te, k, C, out, st);
         stage_end(c, st);
         return s;
     }
@@ -302,9 +357,8 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     // on C1, but the filter time is unchanged (36.2 vs 36.2 ms on A) and the seed costs
     // 1.4-1.8 ms, so it is off by default: the slow path's cost is its per-tile calls on the
     // long tail, not the heap-filling phase.
-    const char* seed_env = getenv("KNN_FILTER_SEED");
     const int64_t ns = std::min<int64_t>(nt, std::min<int64_t>(KNN_SEED_MAX_ROWS, std::max<int64_t>(256, 16 * (int64_t)k)));
-    if (seed_env && atoi(seed_env) == 1 && ns >= k) {
+    if (c->study_seed == 1 && ns >= k) {
         SeedArgs sa{};
         sa.train = tr->feat; sa.nt = nt; sa.ld_t = tr->ld;
         sa.test = te->feat; sa.nq = nq; sa.ld_q = te->ld; sa.d = d; sa.k = k;
@@ -339,7 +393,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         fld_t = fld_q = d;
     }
 
-    const FilterPlan plan = knn_gemm_filter_plan(kelem, rb, k);
+    const FilterPlan plan = knn_gemm_filter_plan(kelem, rb, k, &c->fstudy);
     const int64_t n_qtiles = (nq + plan.bm - 1) / plan.bm;
     const int nseg = choose_splits(c, n_qtiles, nt, kelem, rb, k, cap);
     int64_t seg_len = (nt + nseg - 1) / nseg;
@@ -356,14 +410,14 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     g.cand_L = c->cand_L.as<float>(); g.cand_U = c->cand_U.as<float>(); g.cap = cap; g.cap_seg = cap / nseg;
     // kernel studies: KNN_FILTER_TIMING=1 with a -DKNN_FILTER_TIMING build prints the
     // filter's per-phase shader clocks per wave (wait+barrier, DMA issue, step, slow path)
-    const bool timing = getenv("KNN_FILTER_TIMING") != nullptr;
+    const bool timing = c->study_timing != 0;
     if (timing) {
         HIP_OR_FAIL(c, c->timing.ensure(16 * sizeof(unsigned long long)));
         HIP_OR_FAIL(c, hipMemsetAsync(c->timing.p, 0, 16 * sizeof(unsigned long long), st));
         g.timing = c->timing.as<unsigned long long>();
     }
     stage_begin(c, st, "gemm_filter");
-    HIP_OR_FAIL(c, knn_launch_gemm_filter(g, kelem, rb, st));
+    HIP_OR_FAIL(c, knn_launch_gemm_filter(g, kelem, rb, st, &c->fstudy));
     stage_end(c, st);
     if (timing) {
         unsigned long long t[16];
@@ -398,7 +452,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         }
     }
     stage_begin(c, st, "fallback_scan");
-    knn_status s = run_direct(c, tr, te, k, C, out, st, r.fb_list, r.fb_count);
+    knn_status s = run_exact_scan(c, tr, te, k, C, out, st, r.fb_list, r.fb_count);
     stage_end(c, st);
     return s;
 }
@@ -422,6 +476,11 @@ knn_status knn_create(knn_ctx** out, const knn_opts* opts) {
         c->train_splits = opts->train_splits;
         c->profile = opts->profile;
     }
+    // kernel-study switches (DESIGN.md "Ablation builds"): read here once, never per call
+    if (const char* e = getenv("KNN_FILTER_SEED")) c->study_seed = atoi(e);
+    if (getenv("KNN_FILTER_TIMING")) c->study_timing = 1;
+    if (const char* e = getenv("KNN_FILTER_NBUF")) c->fstudy.nbuf = atoi(e);
+    if (const char* e = getenv("KNN_FILTER_SHAPE")) snprintf(c->fstudy.shape, sizeof(c->fstudy.shape), "%s", e);
     if (c->device < 0 || c->device >= ndev) { delete c; return KNN_ENODEV; }
     hipDeviceProp_t prop;
     if (hipSetDevice(c->device) != hipSuccess || hipGetDeviceProperties(&prop, c->device) != hipSuccess) {
@@ -448,7 +507,7 @@ void knn_destroy(knn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (DBuf* b : {&c->tnorm, &c->tnp, &c->qnorm, &c->gthr, &c->cnt, &c->cand_idx, &c->cand_L, &c->cand_U,
-                    &c->fb_list, &c->ctrl, &c->timing, &c->split_t, &c->split_q, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
+                    &c->fb_list, &c->ctrl, &c->timing, &c->split_t, &c->split_q, &c->seg_rec, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
                     &c->h_dist, &c->h_idx})
         b->release();
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
@@ -506,9 +565,13 @@ knn_status predict_core(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te
             c->stats[4] = 1;
             if ((s = run_gemm(c, tr, te, k, C, out, st, KNN_ALGO_GEMM_SPLIT, &fb)) != KNN_OK) return s;
         }
-    } else {
+    } else if (algo == KNN_ALGO_DIRECT_SCAN) {
         stage_begin(c, st, "exact_scan");
-        if ((s = run_direct(c, tr, te, k, C, out, st, nullptr, nullptr)) != KNN_OK) return s;
+        if ((s = run_exact_scan(c, tr, te, k, C, out, st, nullptr, nullptr)) != KNN_OK) return s;
+        stage_end(c, st);
+    } else {
+        stage_begin(c, st, "direct_tile");
+        if ((s = run_direct_tile(c, tr, te, k, C, out, st)) != KNN_OK) return s;
         stage_end(c, st);
     }
     s = finish_call(c, st);

@@ -63,10 +63,44 @@ struct RescoreArgs {
 
 // Merge of per-shard neighbour lists.  rec: [nsrc][nq][3][k] int32 records (k dist bits,
 // k global indices (-1 = none), k labels), each list ascending by (dist, idx).
+// labels != NULL: the sources are segments of ONE train set (k_direct_tile): indices are
+// its local rows, the vote and out.label read labels[idx] (finish_query).
 struct MergeArgs {
     const int32_t* rec; int nsrc; int64_t nq; int k; int C;
     QueryOut out; int32_t* status;
+    const int32_t* labels;
 };
+
+// class counts up to this many live in a per-wave LDS table; above it the vote runs
+// table-free (vote_ballot), so every path accepts any num_classes
+#define KNN_VOTE_LDS_MAX_C 1024
+// per-wave LDS words of k_merge_vote: class counts, or the k winners' labels + a counter
+__host__ __device__ inline int merge_wave_words(int C, int k) {
+    return C <= KNN_VOTE_LDS_MAX_C ? ((C + 3) & ~3) : ((k + 1 + 3) & ~3);
+}
+
+// k_direct_tile: DT_NW waves per block, 64 train rows per tile, rows staged in chunks of
+// dc <= DT_MAX_DC dims (DT_MAXP 16-B staging registers per thread)
+#define DT_NW 8
+#define DT_MAX_DC 128
+#define DT_MAXP (64 * (DT_MAX_DC / 4) / (64 * DT_NW))
+struct DirectTileArgs {
+    const void* train; const int32_t* labels; int64_t nt; int ld_t;
+    const void* test; int ld_q; int64_t nq;
+    int d; int k; int C; int elem;
+    int64_t seg_len; int nseg; int n_qblocks;
+    int dc; int stride;        // dims per staged chunk (multiple of 4), LDS row stride (floats)
+    int vote_lds;              // per-wave LDS class counts (C <= KNN_VOTE_LDS_MAX_C)
+    QueryOut out; int32_t* status;
+    int32_t* rec;              // nseg > 1: segment records [nseg][nq][3][k] (local rows)
+};
+// queries per k_direct_tile block for k (8 * QW, QW = max(1, 8 / list registers))
+int knn_direct_tile_qb(int k);
+// launch geometry: LDS bytes per block and blocks per CU at that LDS
+size_t knn_direct_tile_lds(int d, int C);
+hipError_t knn_direct_tile_occupancy(int k, int elem, int d, int C, int* blocks_per_cu);
+// fills dc / stride / vote_lds / n_qblocks from d, C, nq and launches nseg * n_qblocks blocks
+hipError_t knn_launch_direct_tile(DirectTileArgs a, hipStream_t st);
 
 struct GenerateArgs {
     void* out; int32_t* labels; int64_t row0; int64_t n; int d; int ld;
@@ -83,10 +117,15 @@ bool knn_gemm_filter_supported(int elem, int row_bytes);
 // groups per wave, row groups per tile, min waves per SIMD (launch bounds), tile buffers,
 // queries per block, LDS bytes per block
 struct FilterPlan { int nw, qg, rg, minw, nbuf, bm; size_t lds; };
-FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k);
-hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st);
-size_t knn_gemm_filter_lds(int elem, int row_bytes, int k);
-hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks_per_cu);
+// kernel-study overrides of the plan (KNN_FILTER_NBUF / KNN_FILTER_SHAPE, read once per
+// context by knn_create); NULL = the product plan
+struct FilterStudy { int nbuf; char shape[8]; };
+FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k, const FilterStudy* fs = nullptr);
+hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st,
+                                  const FilterStudy* fs = nullptr);
+size_t knn_gemm_filter_lds(int elem, int row_bytes, int k, const FilterStudy* fs = nullptr);
+hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks_per_cu,
+                                     const FilterStudy* fs = nullptr);
 // fp32 rows [n][ld] (d % 4 == 0) -> bf16 rows [n][2d]: hi = rn(x), lo = rn(x - hi)
 hipError_t knn_launch_split_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st);
 hipError_t knn_launch_round_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st);

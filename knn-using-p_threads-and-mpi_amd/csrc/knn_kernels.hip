@@ -34,6 +34,7 @@
 #include <type_traits>
 
 #include "knn_kernels.h"
+#include "knn_study.h"
 
 typedef unsigned long long u64;
 static constexpr u64 KEY_NONE = ~0ull;
@@ -175,24 +176,52 @@ __device__ __forceinline__ float direct_dist(const float* q, const E* __restrict
 #pragma clang fp contract(on)
 
 // ---------------------------------------------------------------------------------
+// The vote of main.cpp:64-78 without a C-sized table (any class count): the argmax of
+// the label counts over the list entries, ties to the smallest label.  lab[r] is the
+// label of list element 64r + lane (-1: none / outside the list).  k rounds of one
+// broadcast + R ballots.  Returns (count << 32) | (0xffffffff - label), 0 if empty.
+// ---------------------------------------------------------------------------------
+template <int R>
+__device__ __forceinline__ u64 vote_ballot(const int (&lab)[R], int k) {
+    u64 best = 0;
+    for (int e = 0; e < k; e++) {
+        int le = lab[0];
+#pragma unroll
+        for (int r = 1; r < R; r++)
+            if (r == (e >> 6)) le = lab[r];
+        le = __shfl(le, e & 63);
+        if (le < 0) continue;
+        int cnt = 0;
+#pragma unroll
+        for (int r = 0; r < R; r++) cnt += __popcll(__ballot(lab[r] == le));
+        best = umax64(best, ((u64)(uint32_t)cnt << 32) | (u64)(0xffffffffu - (uint32_t)le));
+    }
+    return best;
+}
+
+// ---------------------------------------------------------------------------------
 // Outputs for one query from a finished wave list: the neighbour list (dist, idx_base +
 // idx, label) and, when o.pred is set, the vote of main.cpp:64-78.
-// counts: wave-private LDS array of C ints.  Runs on one wave.
+// counts: wave-private LDS array of C ints, or NULL for the table-free vote_ballot
+// (class counts above KNN_VOTE_LDS_MAX_C).  Runs on one wave.
 // ---------------------------------------------------------------------------------
 template <int R>
 __device__ void finish_query(const u64 (&T)[R], int k, int C, const int32_t* __restrict__ labels,
                              int* counts, int64_t q, const QueryOut& o, int32_t* __restrict__ status) {
     const int lane = lane_id();
     const bool vote = o.pred != nullptr;
-    if (vote) {
+    const bool lds_vote = vote && counts != nullptr;
+    if (lds_vote) {
         for (int c = lane; c < C; c += 64) counts[c] = 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
     u64 kth = list_at(T, k - 1);
     bool bad = (kth == KEY_NONE);
+    int labr[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
+        labr[r] = -1;
         int e = 64 * r + lane;
         if (e < k) {
             const u64 key = T[r];
@@ -204,7 +233,8 @@ __device__ void finish_query(const u64 (&T)[R], int k, int C, const int32_t* __r
                 if (o.idx) o.idx[off] = (int32_t)(o.idx_base + idx);
                 if (o.label) o.label[off] = lab;
                 if (lab >= 0 && lab < C) {
-                    if (vote) atomicAdd(&counts[lab], 1);
+                    labr[r] = lab;
+                    if (lds_vote) atomicAdd(&counts[lab], 1);
                 } else {
                     atomicOr(status, KNN_STATUS_BAD_LABEL);
                 }
@@ -216,16 +246,20 @@ __device__ void finish_query(const u64 (&T)[R], int k, int C, const int32_t* __r
         }
     }
     if (!vote) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    // argmax, strict '>' scanning 0..C-1 == max count, smallest label on ties
     u64 best = 0;
-    for (int c = lane; c < C; c += 64) {
-        u64 v = ((u64)(uint32_t)counts[c] << 32) | (u64)(0xffffffffu - (uint32_t)c);
-        best = umax64(best, v);
-    }
+    if (lds_vote) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // argmax, strict '>' scanning 0..C-1 == max count, smallest label on ties
+        for (int c = lane; c < C; c += 64) {
+            u64 v = ((u64)(uint32_t)counts[c] << 32) | (u64)(0xffffffffu - (uint32_t)c);
+            best = umax64(best, v);
+        }
 #pragma unroll
-    for (int j = 32; j > 0; j >>= 1) best = umax64(best, __shfl_xor(best, j));
+        for (int j = 32; j > 0; j >>= 1) best = umax64(best, __shfl_xor(best, j));
+    } else {
+        best = vote_ballot<R>(labr, k);
+    }
     if (lane == 0) {
         o.pred[q] = bad ? 0 : (int32_t)(0xffffffffu - (uint32_t)(best & 0xffffffffull));
         if (bad) atomicOr(status, KNN_STATUS_TOO_FEW);
@@ -247,11 +281,10 @@ __global__ __launch_bounds__(256) void k_exact_scan(ExactScanArgs a) {
     float* qs = reinterpret_cast<float*>(smem);
     u64* lists = reinterpret_cast<u64*>(smem + a.q_lds_bytes);
     int* counts = reinterpret_cast<int*>(smem + a.q_lds_bytes + 4 * 64 * R * sizeof(u64));
+    if (a.C > KNN_VOTE_LDS_MAX_C) counts = nullptr;  // table-free vote (vote_ballot)
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
-#if defined(KNN_ABLATE_NO_SLOW) || defined(KNN_ABLATE_NO_EPI) || defined(KNN_ABLATE_NO_DMA) || defined(KNN_STUDY_NO_STORE)
-    if (a.qlist) return;  // ablation builds time the filter only: skip the fallback scan
-#endif
+    KNN_STUDY_SKIP_FALLBACK(a.qlist);
     const int64_t n_work = a.qlist ? (int64_t)(*a.qcount) : a.nq;
     const E* train = reinterpret_cast<const E*>(a.train);
     const E* test = reinterpret_cast<const E*>(a.test);
@@ -295,6 +328,179 @@ __global__ __launch_bounds__(256) void k_exact_scan(ExactScanArgs a) {
         }
     }
 }
+
+// ---------------------------------------------------------------------------------
+// k_direct_tile<QW, R, E>: the direct form (main.cpp:14-23), tiled for throughput.
+// A block of DT_NW = 8 waves owns 8*QW queries: wave w owns QW of them, and lane l
+// computes the distances of train row r0 + l to each of its wave's queries.
+//  * Train tiles (64 rows x DC dims, widened to fp32) are staged once per block in LDS,
+//    double-buffered, and read by all 8 waves: 8*QW queries share every staged byte.
+//    Rows are padded to an odd number of 16-B slots, so the per-lane ds_read_b128 of a
+//    row is conflict-free.  Rows wider than DC are staged in DC-dim chunks; a tile's
+//    partial sums carry over the chunks in ascending dim order.
+//  * Query values are wave-uniform and reach the VALU from scalar loads, so the inner
+//    loop is v_sub (SGPR operand), v_mul, v_add per dim per pair: the reference's
+//    unfused fp32 order, bit for bit (contract(off) below).  VALU-bound: 3 ops per dim
+//    per pair, 128 ops/clk/CU with >= 2 waves per SIMD.
+//  * After each tile every query runs k_exact_scan's selection on its 64 new distances:
+//    a ballot against its running k-th distance (rows of a wave arrive in ascending
+//    order, so `D < k-th distance` is exactly main.cpp:47's strict test), and a wave
+//    bitonic merge only when some lane passes.
+//  * Segments: blockIdx = seg * n_qblocks + qb (co-resident blocks stream the same
+//    rows).  With nseg > 1 each block writes its segment's exact top-k as records
+//    (dist bits, local row, label) [nseg][nq][3][k], merged by k_merge_vote.
+// LDS: 2 tile buffers [64][stride] f32 | per-wave class counts [8][Cpad] (vote_lds)
+// ---------------------------------------------------------------------------------
+#pragma clang fp contract(off)
+template <int QW, int R, typename E>
+__global__ __launch_bounds__(64 * DT_NW, 4) void k_direct_tile(DirectTileArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int NT = 64 * DT_NW;
+    const int lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tile_floats = 64 * a.stride;
+    float* bufs = reinterpret_cast<float*>(smem);
+    int* counts = a.vote_lds ? reinterpret_cast<int*>(smem + 2 * (size_t)tile_floats * 4) + wave * ((a.C + 3) & ~3)
+                             : nullptr;
+    const int qb = blockIdx.x % a.n_qblocks;
+    const int seg = blockIdx.x / a.n_qblocks;
+    const int64_t row_begin = (int64_t)seg * a.seg_len;
+    const int64_t row_end = min(a.nt, row_begin + a.seg_len);
+    const E* __restrict__ train = reinterpret_cast<const E*>(a.train);
+    const E* __restrict__ test = reinterpret_cast<const E*>(a.test);
+    const int d = a.d, k = a.k;
+
+    int64_t qi[QW];
+    const E* qrow[QW];
+    u64 T[QW][R];
+    float thr[QW];
+#pragma unroll
+    for (int i = 0; i < QW; i++) {
+        qi[i] = (int64_t)qb * (DT_NW * QW) + wave * QW + i;
+        qrow[i] = test + (qi[i] < a.nq ? qi[i] : a.nq - 1) * (int64_t)a.ld_q;
+#pragma unroll
+        for (int r = 0; r < R; r++) T[i][r] = KEY_NONE;
+        thr[i] = FLT_MAX;  // main.cpp:33: the FLT_MAX sentinel
+    }
+    const int ngr = (d + 3) >> 2;          // 4-dim groups per row
+    const int gpc = a.dc >> 2;             // groups per chunk
+    const int nchunk = (ngr + gpc - 1) / gpc;
+    const int pieces = 64 * gpc;           // 4-element pieces per staged chunk
+    const int64_t nrows = row_end > row_begin ? row_end - row_begin : 0;
+    const int64_t nsteps = ((nrows + 63) >> 6) * nchunk;
+
+    float4 st[DT_MAXP];
+    auto load_chunk = [&](int64_t s) __attribute__((always_inline)) {
+        const int64_t r0 = row_begin + (s / nchunk) * 64;
+        const int c0 = (int)(s % nchunk) * a.dc;
+#pragma unroll
+        for (int j = 0; j < DT_MAXP; j++) {
+            const int p = threadIdx.x + j * NT;
+            const int row = p / gpc, g = p - row * gpc;
+            if (p < pieces && c0 + 4 * g < 4 * ngr) {
+                const int64_t t = min(r0 + row, row_end - 1);
+                st[j] = load4(train + t * a.ld_t + c0 + 4 * g);
+            }
+        }
+    };
+    auto store_chunk = [&](int64_t s) __attribute__((always_inline)) {
+        float* b = bufs + (s & 1) * tile_floats;
+        const int c0 = (int)(s % nchunk) * a.dc;
+#pragma unroll
+        for (int j = 0; j < DT_MAXP; j++) {
+            const int p = threadIdx.x + j * NT;
+            const int row = p / gpc, g = p - row * gpc;
+            if (p < pieces && c0 + 4 * g < 4 * ngr) *reinterpret_cast<float4*>(b + row * a.stride + 4 * g) = st[j];
+        }
+    };
+
+    float acc[QW];
+#pragma unroll
+    for (int i = 0; i < QW; i++) acc[i] = 0.0f;
+    if (nsteps > 0) {
+        load_chunk(0);
+        store_chunk(0);
+    }
+    __syncthreads();
+    for (int64_t s = 0; s < nsteps; s++) {
+        if (s + 1 < nsteps) load_chunk(s + 1);  // in flight during this chunk's compute
+        const int ch = (int)(s % nchunk);
+        const int c0 = ch * a.dc;
+        const float* tb = bufs + (s & 1) * tile_floats + lane * a.stride;
+        const int gend = min(gpc, ngr - ch * gpc);
+        for (int g = 0; g < gend; g++) {
+            const float4 t = *reinterpret_cast<const float4*>(tb + 4 * g);
+            const int col = c0 + 4 * g;
+            if (col + 4 <= d) {
+#pragma unroll
+                for (int i = 0; i < QW; i++) {
+                    const float4 qv = load4(qrow[i] + col);  // wave-uniform: scalar loads
+                    float s0 = acc[i];
+                    float df;
+                    df = qv.x - t.x; s0 = s0 + df * df;
+                    df = qv.y - t.y; s0 = s0 + df * df;
+                    df = qv.z - t.z; s0 = s0 + df * df;
+                    df = qv.w - t.w; s0 = s0 + df * df;
+                    acc[i] = s0;
+                }
+            } else {
+                const int rem = d - col;  // 1..3 trailing dims
+#pragma unroll
+                for (int i = 0; i < QW; i++) {
+                    const float4 qv = load4(qrow[i] + col);
+                    float s0 = acc[i];
+                    float df;
+                    df = qv.x - t.x; s0 = s0 + df * df;
+                    if (rem > 1) { df = qv.y - t.y; s0 = s0 + df * df; }
+                    if (rem > 2) { df = qv.z - t.z; s0 = s0 + df * df; }
+                    acc[i] = s0;
+                }
+            }
+        }
+        if (ch == nchunk - 1) {
+            // the tile's distances are final: selection (main.cpp:45-61)
+            const int64_t row = row_begin + (s / nchunk) * 64 + lane;
+            const bool valid = row < row_end;
+#pragma unroll
+            for (int i = 0; i < QW; i++) {
+                const bool pass = valid && acc[i] < thr[i];
+                if (__ballot(pass)) {
+                    topk_merge<R>(T[i], pass ? make_key(acc[i], (uint32_t)row) : KEY_NONE);
+                    const u64 kth = list_at(T[i], k - 1);
+                    thr[i] = kth == KEY_NONE ? FLT_MAX : __uint_as_float((uint32_t)(kth >> 32));
+                }
+                acc[i] = 0.0f;
+            }
+        }
+        if (s + 1 < nsteps) store_chunk(s + 1);
+        __syncthreads();
+    }
+    if (a.nseg == 1) {
+#pragma unroll
+        for (int i = 0; i < QW; i++)
+            if (qi[i] < a.nq) finish_query<R>(T[i], k, a.C, a.labels, counts, qi[i], a.out, a.status);
+        return;
+    }
+    // segment records: k (dist bits, local row, label), ascending (KEY_NONE: FLT_MAX, -1, -1)
+#pragma unroll
+    for (int i = 0; i < QW; i++) {
+        if (qi[i] >= a.nq) continue;
+        int32_t* rec = a.rec + ((int64_t)seg * a.nq + qi[i]) * 3 * (int64_t)k;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const int e = 64 * r + lane;
+            if (e < k) {
+                const u64 key = T[i][r];
+                const bool none = key == KEY_NONE;
+                const int32_t idx = (int32_t)(uint32_t)(key & 0xffffffffull);
+                rec[e] = none ? (int32_t)__float_as_uint(FLT_MAX) : (int32_t)(uint32_t)(key >> 32);
+                rec[k + e] = none ? -1 : idx;
+                rec[2 * k + e] = none ? -1 : a.labels[idx];
+            }
+        }
+    }
+}
+#pragma clang fp contract(on)
 
 // ordered uint <-> float (monotone for all non-NaN floats)
 __device__ __forceinline__ uint32_t f2o(float f) {
@@ -464,14 +670,8 @@ __device__ __forceinline__ const void* sgpr_ptr(const void* p) {
 __device__ __forceinline__ void dma16s(uint32_t voff, const void* sbase, uint32_t lds) {
     sbase = sgpr_ptr(sbase);
     lds = __builtin_amdgcn_readfirstlane(lds);
-#ifdef KNN_DMA_PLAIN  // kernel study only: a plain register load of the same bytes (results invalid)
-    uint4 tmp;
-    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(tmp) : "v"(voff), "s"(sbase) : "memory");
-    (void)lds;
-#else
     asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds)
                  : "memory", "m0");
-#endif
 }
 __device__ __forceinline__ void dma4s(uint32_t voff, const void* sbase, uint32_t lds) {
     sbase = sgpr_ptr(sbase);
@@ -792,11 +992,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
         float& th = g1 ? thr[QG - 1] : thr[0];
         if (!(L <= th)) return;
         int& slot = g1 ? ccnt[QG - 1] : ccnt[0];
-#ifndef KNN_STUDY_NO_STORE
         if (slot < cap_sub) {
-#else
-        if (slot < 0) {  // kernel study only: no candidate stores
-#endif
             const int64_t qq = g1 ? q[QG - 1] : q[0];
             const int64_t o = qq * (int64_t)a.cap + (int64_t)(2 * seg + h) * cap_sub + slot;
             a.cand_idx[o] = (int32_t)t;
@@ -1082,11 +1278,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int g = 0; g < QG; g++)
-#ifndef KNN_STUDY_NO_STORE
         if (qvalid[g]) a.cnt[(int64_t)(2 * seg + h) * a.nq + q[g]] = ccnt[g];
-#else
-        if (qvalid[g]) a.cnt[(int64_t)(2 * seg + h) * a.nq + q[g]] = 0;  // nothing stored: rescore skips
-#endif
 #ifdef KNN_FILTER_TIMING
     if (a.timing && lane == 0) {
 #pragma unroll
@@ -1115,7 +1307,7 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
     const int wave = threadIdx.x >> 6;
     unsigned char* my = smem + (size_t)wave * a.wave_lds_bytes;
     float* qs = reinterpret_cast<float*>(my);
-    int* counts = reinterpret_cast<int*>(my + a.q_lds_bytes);
+    int* counts = a.c_lds_bytes ? reinterpret_cast<int*>(my + a.q_lds_bytes) : nullptr;  // NULL: vote_ballot
     int32_t* surv = reinterpret_cast<int32_t*>(my + a.q_lds_bytes + a.c_lds_bytes);
     const int64_t q = (int64_t)blockIdx.x * 4 + wave;
     if (q >= a.nq) return;
@@ -1203,7 +1395,10 @@ __global__ __launch_bounds__(256) void k_merge_vote(MergeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
-    int* counts = reinterpret_cast<int*>(smem) + wave * ((a.C + 3) & ~3);
+    // per-wave LDS: class counts [Cpad] (C <= KNN_VOTE_LDS_MAX_C), else the k winners'
+    // labels [k] + an append counter (vote_ballot)
+    const bool lds_counts = a.C <= KNN_VOTE_LDS_MAX_C;
+    int* counts = reinterpret_cast<int*>(smem) + wave * merge_wave_words(a.C, a.k);
     const int64_t q = (int64_t)blockIdx.x * 4 + wave;
     if (q >= a.nq) return;
     const int k = a.k;
@@ -1227,6 +1422,11 @@ __global__ __launch_bounds__(256) void k_merge_vote(MergeArgs a) {
             }
         }
     }
+    if (a.labels) {
+        // segments of one train set (k_direct_tile): indices are local rows of a.labels
+        finish_query<R>(T, k, a.C, a.labels, lds_counts ? counts : nullptr, q, a.out, a.status);
+        return;
+    }
     const bool bad = (kth == KEY_NONE);
     const QueryOut& o = a.out;
 #pragma unroll
@@ -1236,11 +1436,15 @@ __global__ __launch_bounds__(256) void k_merge_vote(MergeArgs a) {
             const int64_t off = q * o.stride + e;
             const u64 key = T[r];
             if (o.dist) o.dist[off] = key == KEY_NONE ? FLT_MAX : __uint_as_float((uint32_t)(key >> 32));
-            if (o.idx) o.idx[off] = key == KEY_NONE ? -1 : (int32_t)(uint32_t)(key & 0xffffffffull);
+            if (o.idx) o.idx[off] = key == KEY_NONE ? -1 : (int32_t)(o.idx_base + (uint32_t)(key & 0xffffffffull));
         }
     }
     if (!o.pred) return;
-    for (int c = lane; c < a.C; c += 64) counts[c] = 0;
+    if (lds_counts) {
+        for (int c = lane; c < a.C; c += 64) counts[c] = 0;
+    } else if (lane == 0) {
+        counts[k] = 0;  // append counter of the winners' labels
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     for (int s = 0; s < a.nsrc; s++) {
@@ -1251,20 +1455,32 @@ __global__ __launch_bounds__(256) void k_merge_vote(MergeArgs a) {
             const u64 key = make_key(__int_as_float(rec[e]), (uint32_t)ix);
             if (key <= kth && key != KEY_NONE) {
                 const int lab = rec[2 * k + e];
-                if (lab >= 0 && lab < a.C) atomicAdd(&counts[lab], 1);
-                else atomicOr(a.status, KNN_STATUS_BAD_LABEL);
+                if (lab >= 0 && lab < a.C) {
+                    if (lds_counts) atomicAdd(&counts[lab], 1);
+                    else counts[atomicAdd(&counts[k], 1)] = lab;
+                } else {
+                    atomicOr(a.status, KNN_STATUS_BAD_LABEL);
+                }
             }
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
     u64 best = 0;
-    for (int c = lane; c < a.C; c += 64) {
-        u64 v = ((u64)(uint32_t)counts[c] << 32) | (u64)(0xffffffffu - (uint32_t)c);
-        best = umax64(best, v);
-    }
+    if (lds_counts) {
+        for (int c = lane; c < a.C; c += 64) {
+            u64 v = ((u64)(uint32_t)counts[c] << 32) | (u64)(0xffffffffu - (uint32_t)c);
+            best = umax64(best, v);
+        }
 #pragma unroll
-    for (int j = 32; j > 0; j >>= 1) best = umax64(best, __shfl_xor(best, j));
+        for (int j = 32; j > 0; j >>= 1) best = umax64(best, __shfl_xor(best, j));
+    } else {
+        const int nw = counts[k];
+        int labr[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) labr[r] = (64 * r + lane < nw) ? counts[64 * r + lane] : -1;
+        best = vote_ballot<R>(labr, k);
+    }
     if (lane == 0) {
         o.pred[q] = bad ? 0 : (int32_t)(0xffffffffu - (uint32_t)(best & 0xffffffffull));
         if (bad) atomicOr(a.status, KNN_STATUS_TOO_FEW);
@@ -1355,7 +1571,8 @@ template <int R, typename E>
 static hipError_t launch_exact_r(const ExactScanArgs& a0, int grid, hipStream_t st) {
     ExactScanArgs a = a0;
     a.q_lds_bytes = (int)align16((size_t)a.d * sizeof(float));
-    size_t lds = a.q_lds_bytes + 4 * 64 * R * sizeof(u64) + align16((size_t)a.C * sizeof(int));
+    size_t lds = a.q_lds_bytes + 4 * 64 * R * sizeof(u64) +
+                 (a.C <= KNN_VOTE_LDS_MAX_C ? align16((size_t)a.C * sizeof(int)) : 0);
     hipLaunchKernelGGL((k_exact_scan<R, E>), dim3(grid), dim3(256), lds, st, a);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
@@ -1377,7 +1594,66 @@ hipError_t knn_launch_exact_scan(const ExactScanArgs& a, int grid, hipStream_t s
 }
 
 size_t knn_exact_scan_lds(int d, int k, int C) {
-    return align16((size_t)d * 4) + 4 * 64 * (size_t)list_regs(k) * 8 + align16((size_t)C * 4);
+    return align16((size_t)d * 4) + 4 * 64 * (size_t)list_regs(k) * 8 +
+           (C <= KNN_VOTE_LDS_MAX_C ? align16((size_t)C * 4) : 0);
+}
+
+// ---- k_direct_tile ----
+// QW queries per wave: 8 / list registers (the wave lists T[QW][R] stay at 16 VGPRs)
+static int direct_qw(int k) { return std::max(1, 8 / list_regs(k)); }
+int knn_direct_tile_qb(int k) { return DT_NW * direct_qw(k); }
+
+// dims per staged chunk and the padded LDS row stride (an odd number of 16-B slots)
+static void direct_tile_geom(int d, int* dc, int* stride) {
+    const int dpad = (d + 3) & ~3;
+    *dc = std::min(dpad, DT_MAX_DC);
+    int slots = *dc / 4;
+    if ((slots & 1) == 0) slots++;
+    *stride = 4 * slots;
+}
+
+size_t knn_direct_tile_lds(int d, int C) {
+    int dc, stride;
+    direct_tile_geom(d, &dc, &stride);
+    return 2 * 64 * (size_t)stride * 4 + (C <= KNN_VOTE_LDS_MAX_C ? (size_t)DT_NW * ((C + 3) & ~3) * 4 : 0);
+}
+
+template <int QW, int R, typename E>
+static const void* direct_tile_fn() { return reinterpret_cast<const void*>(&k_direct_tile<QW, R, E>); }
+
+template <typename E>
+static const void* direct_tile_fn_e(int k) {
+    switch (list_regs(k)) {
+        case 1: return direct_tile_fn<8, 1, E>();
+        case 2: return direct_tile_fn<4, 2, E>();
+        case 4: return direct_tile_fn<2, 4, E>();
+        case 8: return direct_tile_fn<1, 8, E>();
+        default: return direct_tile_fn<1, 16, E>();
+    }
+}
+static const void* direct_tile_ptr(int k, int elem) {
+    return elem == ELEM_BF16 ? direct_tile_fn_e<bf16_t>(k) : direct_tile_fn_e<float>(k);
+}
+
+hipError_t knn_direct_tile_occupancy(int k, int elem, int d, int C, int* blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, direct_tile_ptr(k, elem), 64 * DT_NW,
+                                                        knn_direct_tile_lds(d, C));
+}
+
+hipError_t knn_launch_direct_tile(DirectTileArgs a, hipStream_t st) {
+    if (a.nq <= 0) return hipSuccess;
+    if (a.nseg < 1 || (a.nseg > 1 && !a.rec) || a.d < 1 || a.k < 1 || a.k > 1024) return hipErrorInvalidValue;
+    direct_tile_geom(a.d, &a.dc, &a.stride);
+    a.vote_lds = a.C <= KNN_VOTE_LDS_MAX_C;
+    const int qb = knn_direct_tile_qb(a.k);
+    a.n_qblocks = (int)((a.nq + qb - 1) / qb);
+    const dim3 grid((unsigned)((int64_t)a.n_qblocks * a.nseg));
+    void* args[] = {&a};
+    hipError_t e = hipLaunchKernel(direct_tile_ptr(a.k, a.elem), grid, dim3(64 * DT_NW), args,
+                                   knn_direct_tile_lds(a.d, a.C), st);
+    if (e != hipSuccess) return e;
+    KNN_LAUNCH_CHECK();
+    return hipSuccess;
 }
 
 hipError_t knn_launch_row_norms(const void* x, int elem, int64_t n, int ld, int d, float* out,
@@ -1413,12 +1689,10 @@ static size_t gemm_filter_lds_of(int row_bytes, int k, int nw, int qg, int rg, i
 //    Larger k that does not fit falls back to the fp32 shape.
 //  bf16 rows of 128 bytes (64 features): 4 waves x 32 queries, 64-row tiles, two blocks per CU.
 // KNN_FILTER_NBUF=2|3 and KNN_FILTER_SHAPE=w8r2|w8|w4r1|w4q2|w4 (bf16/split) force a shape (kernel studies).
-FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k) {
+FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k, const FilterStudy* fs) {
     const size_t cap = 160 * 1024;
-    const char* env_nb = getenv("KNN_FILTER_NBUF");
-    const char* env_sh = getenv("KNN_FILTER_SHAPE");
-    const int force_nb = env_nb ? atoi(env_nb) : 0;
-    const std::string shape = env_sh ? env_sh : "";
+    const int force_nb = fs ? fs->nbuf : 0;
+    const std::string shape = fs ? fs->shape : "";
     auto fits = [&](int nw, int qg, int rg, int nbuf, size_t limit) {
         return gemm_filter_lds_of(row_bytes, k, nw, qg, rg, nbuf) <= limit;
     };
@@ -1460,7 +1734,9 @@ FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k) {
     return make(4, 1, 2, 1, 2);
 }
 
-size_t knn_gemm_filter_lds(int elem, int row_bytes, int k) { return knn_gemm_filter_plan(elem, row_bytes, k).lds; }
+size_t knn_gemm_filter_lds(int elem, int row_bytes, int k, const FilterStudy* fs) {
+    return knn_gemm_filter_plan(elem, row_bytes, k, fs).lds;
+}
 
 bool knn_gemm_filter_supported(int elem, int row_bytes) {
     (void)elem;
@@ -1492,16 +1768,17 @@ static const void* gemm_filter_ptr(int elem, int row_bytes, const FilterPlan& f)
          : row_bytes == 256 ? gemm_filter_fn<float, 256>(f) : gemm_filter_fn<float, 512>(f);
 }
 
-hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks_per_cu) {
+hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks_per_cu, const FilterStudy* fs) {
     if (!knn_gemm_filter_supported(elem, row_bytes)) return hipErrorInvalidValue;
-    const FilterPlan f = knn_gemm_filter_plan(elem, row_bytes, k);
+    const FilterPlan f = knn_gemm_filter_plan(elem, row_bytes, k, fs);
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, gemm_filter_ptr(elem, row_bytes, f),
                                                         64 * f.nw, f.lds);
 }
 
-hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st) {
+hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st,
+                                  const FilterStudy* fs) {
     if (!knn_gemm_filter_supported(elem, row_bytes)) return hipErrorInvalidValue;
-    const FilterPlan f = knn_gemm_filter_plan(elem, row_bytes, a.k);
+    const FilterPlan f = knn_gemm_filter_plan(elem, row_bytes, a.k, fs);
     const void* fn = gemm_filter_ptr(elem, row_bytes, f);
     void* args[] = {const_cast<GemmFilterArgs*>(&a)};
     const dim3 grid((unsigned)(a.n_qtiles * a.nseg));
@@ -1515,7 +1792,7 @@ template <int R, typename E>
 static hipError_t launch_rescore_r(const RescoreArgs& a0, hipStream_t st) {
     RescoreArgs a = a0;
     a.q_lds_bytes = (int)align16((size_t)a.d * 4);
-    a.c_lds_bytes = (int)align16((size_t)a.C * 4);
+    a.c_lds_bytes = a.C <= KNN_VOTE_LDS_MAX_C ? (int)align16((size_t)a.C * 4) : 0;
     a.wave_lds_bytes = a.q_lds_bytes + a.c_lds_bytes + 64 * KNN_RESCORE_CAPW * 4;
     size_t lds = 4 * (size_t)a.wave_lds_bytes;
     unsigned grid = (unsigned)((a.nq + 3) / 4);
@@ -1607,7 +1884,7 @@ template <int R>
 static hipError_t launch_merge_r(const MergeArgs& a, hipStream_t st) {
     const unsigned grid = (unsigned)((a.nq + 3) / 4);
     if (grid == 0) return hipSuccess;
-    const size_t lds = 4 * (size_t)((a.C + 3) & ~3) * sizeof(int);
+    const size_t lds = 4 * (size_t)merge_wave_words(a.C, a.k) * sizeof(int);
     hipLaunchKernelGGL(k_merge_vote<R>, dim3(grid), dim3(256), lds, st, a);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
