@@ -149,8 +149,9 @@ int32_t knn_stage_times(const knn_ctx* ctx, const char** names, float* ms, int32
 /* Counters of the last predict call: [0] GEMM candidates kept, [1] queries sent to
  * the exact fallback, [2] train segments used, [3] filter operand type (-1 = no GEMM
  * filter ran, 0 = fp32, 1 = bf16, 2 = bf16 hi/lo split of fp32, 3 = bf16 rounding of
- * fp32), [4] 1 when AUTO re-ran the call with the split filter.  Returns the number
- * written. */
+ * fp32), [4] 1 when AUTO re-ran the call with the split filter, [5] 1 when the filter
+ * ran with the train norm folded into the MFMA (the fused-norm bf16 filter).  Returns the
+ * number written. */
 int32_t knn_last_stats(const knn_ctx* ctx, int64_t* out, int32_t n);
 
 /*
@@ -179,6 +180,14 @@ float knn_accuracy(const int32_t* cm, int32_t num_classes, int64_t n);
 knn_status knn_confusion_matrix_device(knn_ctx* ctx, const int32_t* d_pred, const int32_t* d_labels,
                                        int64_t n, int32_t num_classes, int32_t* d_cm,
                                        int64_t* d_correct, void* hip_stream);
+
+/* Self-test of the hardware assumption behind the bf16 GEMM-form certificate (no
+ * reference counterpart; DESIGN.md "Certificate"): runs the bf16 filter's MFMA chain
+ * (v_mfma_f32_32x32x16_bf16 over K/16 k-steps, the filter's lane map) on device
+ * operands a, b = [32][K] bf16 bits (K % 16 == 0) and writes d_out[i][j] =
+ * sum_k a[i][k] b[j][k] as the MFMA accumulates it (device float [32][32]). */
+knn_status knn_mfma_probe_bf16(knn_ctx* ctx, const uint16_t* d_a, const uint16_t* d_b, int32_t K,
+                               float* d_out, void* hip_stream);
 
 /* ARFF loader (replaces ArffParser::parse, libarff/arff_parser.cpp:23, for the
  * read path): NUMERIC attributes parsed with libarff's istringstream>>float rules.

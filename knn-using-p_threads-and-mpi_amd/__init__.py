@@ -87,6 +87,7 @@ def load_library(path=LIB_PATH):
         "knn_last_stats": (I32, [P, ctypes.POINTER(I64), I32]),
         "knn_generate": (I32, [P, P, P, I64, I64, I32, I32, I32, I32, ctypes.c_uint64,
                                ctypes.c_uint32, I32, P]),
+        "knn_mfma_probe_bf16": (I32, [P, P, P, I32, P, P]),
         "knn_confusion_matrix": (I32, [P, P, I64, I32, P]),
         "knn_confusion_matrix_device": (I32, [P, P, P, I64, I32, P, P, P]),
         "knn_accuracy": (F, [P, I32, I64]),
@@ -368,6 +369,18 @@ class Context:
         n = pred.shape[0]
         return cm, float(np.float32(int(corr.item())) / np.float32(n)) if n else float("nan")
 
+    def mfma_probe_bf16(self, a, b, stream=None):
+        """The bf16 filter's MFMA chain on device operands a, b: [32][K] torch.bfloat16
+        (K % 16 == 0) -> float32 [32][32] = a @ b.T as v_mfma_f32_32x32x16_bf16 sums it."""
+        import torch
+        if a.shape != b.shape or a.dim() != 2 or a.shape[0] != 32 or a.dtype != torch.bfloat16:
+            raise KnnError(KNN_EINVAL, "a, b must be [32][K] bfloat16")
+        a, b = a.contiguous(), b.contiguous()
+        out = torch.empty((32, 32), dtype=torch.float32, device=a.device)
+        self._check(self.lib.knn_mfma_probe_bf16(self.h, a.data_ptr(), b.data_ptr(), a.shape[1], out.data_ptr(),
+                                                 None if stream is None else ctypes.c_void_p(stream)))
+        return out
+
     def stage_times(self):
         names = (ctypes.c_char_p * 16)()
         ms = (ctypes.c_float * 16)()
@@ -379,10 +392,11 @@ class Context:
         return out
 
     def stats(self):
-        v = (ctypes.c_int64 * 5)()
-        self.lib.knn_last_stats(self.h, v, 5)
+        v = (ctypes.c_int64 * 6)()
+        self.lib.knn_last_stats(self.h, v, 6)
         return {"candidates": v[0], "fallback_queries": v[1], "train_segments": v[2],
-                "filter_operands": FILTER_OPERANDS.get(v[3], v[3]), "rerun_split": bool(v[4])}
+                "filter_operands": FILTER_OPERANDS.get(v[3], v[3]), "rerun_split": bool(v[4]),
+                "fused_norm": bool(v[5])}
 
 
 _default_ctx = None

@@ -61,8 +61,9 @@ struct knn_ctx {
     DBuf tnorm, tnp, qnorm, gthr, cnt, cand_idx, cand_L, cand_U, fb_list, ctrl, timing;
     DBuf split_t, split_q;  // KNN_ALGO_GEMM_SPLIT / _BF16: bf16 [hi | lo] / rn copies of fp32 rows
     DBuf seg_rec;           // k_direct_tile segment records [nseg][nq][3][k]
+    DBuf tmax;              // fused filter: per-64-row maximum train norm
     // kernel-study switches, read once from the environment in knn_create (never in a call)
-    int study_seed = 0, study_timing = 0;
+    int study_seed = 0, study_timing = 0, study_nofused = 0;
     FilterStudy fstudy{0, {0}};
     // host-API staging (device copies of host inputs / outputs)
     DBuf h_train, h_labels, h_test, h_pred, h_dist, h_idx;
@@ -72,7 +73,7 @@ struct knn_ctx {
     std::vector<Stage> stages;
     std::vector<float> stage_ms;
     std::vector<const char*> stage_names;
-    int64_t stats[5] = {0, 0, 0, -1, 0};  // candidates, fallback queries, segments, filter operand type, rerun
+    int64_t stats[6] = {0, 0, 0, -1, 0, 0};  // candidates, fallback queries, segments, filter operand type, rerun, fused
     int num_cus = 256;
 };
 
@@ -281,7 +282,24 @@ void certificate(int d, int felem, float* coef, float* eta) {
     }
 }
 
-int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int rb, int k, int cap) {
+// Fused-norm filter (knn_fused.hip): y = fl_mfma(sum -2 rq_i rt_i + tn_hi + tn_mid + tn_lo),
+// G = fl(qn + y), Delta = coef (qn + tn) + eta; rq, rt = the bf16 operands (q, t themselves
+// for bf16 data, rn(q), rn(t) for fp32 data).  With N = qn + tn (exact norms):
+//   MFMA accumulation of d + 3 terms at <= 2u per add, terms summing to <= 2.01 N: 4.02 (d+3) u N
+//   tn split hi + mid + lo (each subtraction exact): <= 2^-24 tn <= u N
+//   fp32 norms (fmaf chains): <= 1.01 d u each, 2.02 d u N;  G's rounding: <= 3.01 u N
+//   the reference's D vs the exact distance: <= 2 (d+2) u N
+// -> (8.04 d + 20.1) u N; the roundings of s, coef s, L and U and slack in 512 u N:
+//   bf16 data: coef = (9d + 512) u.  Rounded fp32 data adds the operand rounding,
+//   2 sum |q_i t_i - rn(q_i) rn(t_i)| <= (2^-7 + 2^-16) N = 131328 u N: coef = (9d + 131840) u.
+// eta (products or partial sums flushed to zero, subnormal operand rounding): (8d + 16) 2^-125.
+void certificate_fused(int d, bool rounded, float* coef, float* eta) {
+    *coef = (float)(9 * d + (rounded ? 131840 : 512)) * 0x1p-24f;
+    *eta = (float)(8 * d + 16) * 0x1p-125f;
+}
+
+int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int rb, int k, int cap,
+                  bool fused = false, int d = 0) {
     if (c->train_splits > 0) return std::min(8, c->train_splits);
     // More segments shrink the partial last wave of blocks (measured on config A:
     // S=3 224 ms, S=5 217 ms, S=8 216 ms), but each segment must fit its rows in its
@@ -290,7 +308,9 @@ int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int
     // tile; the slice gets a 1.5x margin.  Overflowing queries still finish exactly,
     // on the slow full-scan fallback.
     int occ = 1;
-    if (knn_gemm_filter_occupancy(dtype, rb, k, &occ, &c->fstudy) != hipSuccess || occ < 1) occ = 1;
+    const hipError_t oe = fused ? knn_fused_occupancy(d, k, &occ, &c->fstudy)
+                                : knn_gemm_filter_occupancy(dtype, rb, k, &occ, &c->fstudy);
+    if (oe != hipSuccess || occ < 1) occ = 1;
     const int64_t slots = (int64_t)occ * c->num_cus;
     int best = 1;
     double best_eff = 0.0;
@@ -327,12 +347,20 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     HIP_OR_FAIL(c, c->cand_U.ensure(sizeof(float) * nq * cap));
     HIP_OR_FAIL(c, c->fb_list.ensure(sizeof(int32_t) * nq));
 
+    // bf16 MFMA operands (rounded fp32 rows or bf16 data) run the fused-norm filter
+    const bool fused = !c->study_nofused && (felem == ELEM_ROUND || felem == ELEM_BF16) &&
+                       knn_fused_supported(d) && knn_fused_plan(d, k, &c->fstudy).nw > 0;
     float coef, eta;
-    certificate(d, felem, &coef, &eta);
+    if (fused) {
+        certificate_fused(d, felem == ELEM_ROUND, &coef, &eta);
+        HIP_OR_FAIL(c, c->tmax.ensure(sizeof(float) * ((nt + 63) / 64 + 1)));
+    } else {
+        certificate(d, felem, &coef, &eta);
+    }
     stage_begin(c, st, "norms");
     HIP_OR_FAIL(c, knn_launch_row_norms(tr->feat, dtype, nt, tr->ld, d, c->tnorm.as<float>(),
                                         c->ctrl.as<int32_t>(), c->ctrl.as<uint32_t>() + 2,
-                                        c->tnp.as<float>(), 1.0f - coef, st));
+                                        c->tnp.as<float>(), 1.0f - coef, st, fused ? c->tmax.as<float>() : nullptr));
     HIP_OR_FAIL(c, knn_launch_row_norms(te->feat, dtype, nq, te->ld, d, c->qnorm.as<float>(),
                                         c->ctrl.as<int32_t>(), nullptr, nullptr, 0.0f, st));
     stage_end(c, st);
@@ -373,7 +401,19 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     const void* ftrain = tr->feat;
     const void* ftest = te->feat;
     int fld_t = tr->ld, fld_q = te->ld;
-    if (felem == ELEM_SPLIT) {
+    if (fused) {
+        // augmented bf16 rows: train [rn(t) | tn split], queries [-2 rn(q) | 1 1 1]
+        HIP_OR_FAIL(c, c->split_t.ensure(sizeof(uint16_t) * (size_t)(d + 16) * nt));
+        HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * (size_t)(d + 16) * nq));
+        stage_begin(c, st, "aug");
+        HIP_OR_FAIL(c, knn_launch_aug_rows(tr->feat, dtype, nt, tr->ld, d, c->tnorm.as<float>(), 1.0f,
+                                           c->split_t.as<uint16_t>(), st));
+        HIP_OR_FAIL(c, knn_launch_aug_rows(te->feat, dtype, nq, te->ld, d, nullptr, -2.0f,
+                                           c->split_q.as<uint16_t>(), st));
+        stage_end(c, st);
+        ftrain = c->split_t.p; ftest = c->split_q.p;
+        fld_t = fld_q = d + 16;
+    } else if (felem == ELEM_SPLIT) {
         HIP_OR_FAIL(c, c->split_t.ensure(sizeof(uint16_t) * 2 * d * nt));
         HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * 2 * d * nq));
         stage_begin(c, st, "split");
@@ -393,9 +433,9 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         fld_t = fld_q = d;
     }
 
-    const FilterPlan plan = knn_gemm_filter_plan(kelem, rb, k, &c->fstudy);
+    const FilterPlan plan = fused ? knn_fused_plan(d, k, &c->fstudy) : knn_gemm_filter_plan(kelem, rb, k, &c->fstudy);
     const int64_t n_qtiles = (nq + plan.bm - 1) / plan.bm;
-    const int nseg = choose_splits(c, n_qtiles, nt, kelem, rb, k, cap);
+    const int nseg = choose_splits(c, n_qtiles, nt, kelem, rb, k, cap, fused, d);
     int64_t seg_len = (nt + nseg - 1) / nseg;
     seg_len = (seg_len + 63) / 64 * 64;
     GemmFilterArgs g{};
@@ -408,6 +448,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     g.gthr = c->gthr.as<uint32_t>();
     g.cnt = c->cnt.as<int32_t>(); g.cand_idx = c->cand_idx.as<int32_t>();
     g.cand_L = c->cand_L.as<float>(); g.cand_U = c->cand_U.as<float>(); g.cap = cap; g.cap_seg = cap / nseg;
+    g.tmax = fused ? c->tmax.as<float>() : nullptr;
     // kernel studies: KNN_FILTER_TIMING=1 with a -DKNN_FILTER_TIMING build prints the
     // filter's per-phase shader clocks per wave (wait+barrier, DMA issue, step, slow path)
     const bool timing = c->study_timing != 0;
@@ -417,7 +458,8 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         g.timing = c->timing.as<unsigned long long>();
     }
     stage_begin(c, st, "gemm_filter");
-    HIP_OR_FAIL(c, knn_launch_gemm_filter(g, kelem, rb, st, &c->fstudy));
+    if (fused) HIP_OR_FAIL(c, knn_launch_fused(g, st, &c->fstudy));
+    else HIP_OR_FAIL(c, knn_launch_gemm_filter(g, kelem, rb, st, &c->fstudy));
     stage_end(c, st);
     if (timing) {
         unsigned long long t[16];
@@ -425,7 +467,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         HIP_OR_FAIL(c, hipStreamSynchronize(st));
         const double w = t[4] ? (double)t[4] : 1.0;
         fprintf(stderr, "[knn filter timing] waves=%llu clocks/wave: wait+barrier %.4g  dma %.4g  step %.4g  slow %.4g"
-                " (after tile 4096: %.4g; calls %.4g, mask %.4g, turns %.4g)\n", t[4], t[0] / w, t[1] / w,
+                " ([5] %.4g; [6] %.4g, [7] %.4g, [8] %.4g)\n", t[4], t[0] / w, t[1] / w,
                 t[2] / w, t[3] / w, t[5] / w, t[6] / w, t[7] / w, t[8] / w);
     }
 
@@ -442,6 +484,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
 
     c->stats[2] = nseg;
     c->stats[3] = felem;
+    c->stats[5] = fused;
     if (retry_limit >= 0) {
         // AUTO's rounded filter: too many overflowing queries -> the caller re-runs as split
         HIP_OR_FAIL(c, hipMemcpyAsync(c->ctrl_host, c->ctrl.p, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
@@ -479,6 +522,7 @@ knn_status knn_create(knn_ctx** out, const knn_opts* opts) {
     // kernel-study switches (DESIGN.md "Ablation builds"): read here once, never per call
     if (const char* e = getenv("KNN_FILTER_SEED")) c->study_seed = atoi(e);
     if (getenv("KNN_FILTER_TIMING")) c->study_timing = 1;
+    if (const char* e = getenv("KNN_FILTER_FUSED")) c->study_nofused = atoi(e) == 0;
     if (const char* e = getenv("KNN_FILTER_NBUF")) c->fstudy.nbuf = atoi(e);
     if (const char* e = getenv("KNN_FILTER_SHAPE")) snprintf(c->fstudy.shape, sizeof(c->fstudy.shape), "%s", e);
     if (c->device < 0 || c->device >= ndev) { delete c; return KNN_ENODEV; }
@@ -507,7 +551,7 @@ void knn_destroy(knn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (DBuf* b : {&c->tnorm, &c->tnp, &c->qnorm, &c->gthr, &c->cnt, &c->cand_idx, &c->cand_L, &c->cand_U,
-                    &c->fb_list, &c->ctrl, &c->timing, &c->split_t, &c->split_q, &c->seg_rec, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
+                    &c->fb_list, &c->ctrl, &c->timing, &c->split_t, &c->split_q, &c->seg_rec, &c->tmax, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
                     &c->h_dist, &c->h_idx})
         b->release();
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
@@ -546,7 +590,7 @@ knn_status predict_core(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te
     HIP_OR_FAIL(c, hipSetDevice(c->device));
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
     c->stages.clear();
-    c->stats[0] = c->stats[1] = c->stats[2] = c->stats[4] = 0;
+    c->stats[0] = c->stats[1] = c->stats[2] = c->stats[4] = c->stats[5] = 0;
     c->stats[3] = -1;
     if (te->n == 0) return KNN_OK;
     HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st));
@@ -693,7 +737,7 @@ int32_t knn_stage_times(const knn_ctx* c, const char** names, float* ms, int32_t
 
 int32_t knn_last_stats(const knn_ctx* c, int64_t* out, int32_t n) {
     if (!c || !out) return 0;
-    int32_t m = std::min(n, 5);
+    int32_t m = std::min(n, 6);
     for (int32_t i = 0; i < m; i++) out[i] = c->stats[i];
     return m;
 }
@@ -710,6 +754,18 @@ knn_status knn_generate(knn_ctx* c, void* d_feat, int32_t* d_labels, int64_t row
     GenerateArgs a{d_feat, d_labels, row0, n, d, ld, dtype == KNN_BF16, kind, seed, stream, C};
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
     HIP_OR_FAIL(c, knn_launch_generate(a, st));
+    HIP_OR_FAIL(c, hipStreamSynchronize(st));
+    return KNN_OK;
+}
+
+knn_status knn_mfma_probe_bf16(knn_ctx* c, const uint16_t* d_a, const uint16_t* d_b, int32_t K, float* d_out,
+                               void* hip_stream) {
+    if (!c) return KNN_EINVAL;
+    c->err.clear();
+    if (K <= 0 || K % 16 || !d_a || !d_b || !d_out) return fail(c, KNN_EINVAL, "mfma probe: K must be a positive multiple of 16");
+    HIP_OR_FAIL(c, hipSetDevice(c->device));
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    HIP_OR_FAIL(c, knn_launch_mfma_probe(d_a, d_b, K, d_out, st));
     HIP_OR_FAIL(c, hipStreamSynchronize(st));
     return KNN_OK;
 }

@@ -1,0 +1,201 @@
+// knn_device.h -- device helpers shared by the kernel translation units of libknn_amd
+// (knn_kernels.hip, knn_fused.hip): keys and wave bitonic networks, bf16 helpers,
+// ordered-float bits, LDS-DMA issue and the GEMM filter tile geometry.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <stdint.h>
+
+#include "knn_kernels.h"
+
+typedef unsigned long long u64;
+#define KNN_LAUNCH_CHECK() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return e_; } while (0)
+static constexpr u64 KEY_NONE = ~0ull;
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+#ifndef KNN_FILTER_PK
+#define KNN_FILTER_PK 0
+#endif
+
+// ---------------------------------------------------------------------------------
+// Keys and wave-level bitonic networks (64 lanes, one element per lane per register)
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ u64 make_key(float dist, uint32_t idx) {
+    if (!(dist < FLT_MAX)) return KEY_NONE;  // main.cpp:47 against the FLT_MAX sentinel
+    return ((u64)__float_as_uint(dist) << 32) | (u64)idx;
+}
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+__device__ __forceinline__ u64 umin64(u64 a, u64 b) { return a < b ? a : b; }
+__device__ __forceinline__ u64 umax64(u64 a, u64 b) { return a < b ? b : a; }
+
+// compare-exchange with lane ^ j; keep the smaller key if keep_min
+__device__ __forceinline__ u64 cx(u64 v, int j, bool keep_min) {
+    u64 o = __shfl_xor(v, j);
+    return keep_min ? umin64(v, o) : umax64(v, o);
+}
+
+// full bitonic sort of 64 keys across the wave
+__device__ __forceinline__ u64 sort64(u64 v, bool descending) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+        for (int j = size >> 1; j > 0; j >>= 1) {
+            bool up = ((lane & size) == 0) != descending;
+            bool lower = (lane & j) == 0;
+            v = cx(v, j, lower == up);
+        }
+    }
+    return v;
+}
+
+// bitonic merge of a bitonic 64-sequence
+__device__ __forceinline__ u64 merge64(u64 v, bool ascending) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int j = 32; j > 0; j >>= 1) v = cx(v, j, ((lane & j) == 0) == ascending);
+    return v;
+}
+
+// Wave-resident sorted list of the 64*R smallest keys: element e = 64*r + lane lives in
+// T[r] of lane (e & 63).  Merge one batch of 64 new keys (one per lane).
+template <int R>
+__device__ __forceinline__ void topk_merge(u64 (&T)[R], u64 x) {
+    x = sort64(x, /*descending=*/true);
+    u64 y = umin64(T[R - 1], x);  // half-cleaner: the 64 smallest of T[R-1] u x, bitonic
+    if constexpr (R == 1) {
+        T[0] = merge64(y, true);
+    } else {
+        // [T0..T(R-2) ascending, T(R-1) descending] is bitonic over 64R elements
+        T[R - 1] = merge64(y, false);
+#pragma unroll
+        for (int s = R / 2; s >= 1; s >>= 1) {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                if ((r & s) == 0) {
+                    u64 a = T[r], b = T[r + s];
+                    T[r] = umin64(a, b);
+                    T[r + s] = umax64(a, b);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) T[r] = merge64(T[r], true);
+    }
+}
+
+// element e of the wave list, broadcast to every lane
+template <int R>
+__device__ __forceinline__ u64 list_at(const u64 (&T)[R], int e) {
+    u64 v = T[0];
+#pragma unroll
+    for (int r = 1; r < R; r++)
+        if (r == (e >> 6)) v = T[r];
+    return __shfl(v, e & 63);
+}
+
+// ---------------------------------------------------------------------------------
+// Feature elements: fp32, or bf16 bits widened exactly (bf16 -> fp32 is a 16-bit shift)
+// ---------------------------------------------------------------------------------
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+// filter operand tag for ELEM_SPLIT rows (bf16 bits [hi(d) | lo(d)] of fp32 data)
+struct split_t { uint16_t v; };
+
+// fp32 -> bf16 bits, round to nearest even (finite inputs)
+__device__ __forceinline__ uint32_t bf16_rne(float x) {
+    const uint32_t b = __float_as_uint(x);
+    return (b + 0x7fffu + ((b >> 16) & 1u)) >> 16;
+}
+
+__device__ __forceinline__ float widen(float v) { return v; }
+__device__ __forceinline__ float widen(bf16_t v) { return __uint_as_float((uint32_t)v << 16); }
+
+// four consecutive elements as fp32 (p aligned to 4 elements)
+__device__ __forceinline__ float4 load4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 load4(const bf16_t* p) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    return make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
+                       __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u));
+}
+
+// ordered uint <-> float (monotone for all non-NaN floats)
+__device__ __forceinline__ uint32_t f2o(float f) {
+    uint32_t b = __float_as_uint(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float o2f(uint32_t o) {
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+
+__device__ __forceinline__ float f4get(const float4& v, int i) {
+    return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+}
+__device__ __forceinline__ float u4getf(const uint4& v, int i) {
+    return __uint_as_float(i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w);
+}
+
+// LDS-DMA issued by inline asm: the compiler does not see these as LDS writes, so it
+// does not put a vmcnt(0) in front of the next LDS read (which would serialise every
+// tile's compute behind the DMA of the tile after it); the kernel orders them itself
+// with counted waits + s_barrier (wait_dma_barrier).  M0 = LDS destination (uniform).
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds) {
+    lds = __builtin_amdgcn_readfirstlane(lds);
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(lds)
+                 : "memory", "m0");
+}
+// a wave-uniform value the compiler may have kept in VGPRs, as SGPRs
+__device__ __forceinline__ const void* sgpr_ptr(const void* p) {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (const void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+// scalar base + 32-bit per-lane offset (no per-lane 64-bit address math in the loop)
+__device__ __forceinline__ void dma16s(uint32_t voff, const void* sbase, uint32_t lds) {
+    sbase = sgpr_ptr(sbase);
+    lds = __builtin_amdgcn_readfirstlane(lds);
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds)
+                 : "memory", "m0");
+}
+__device__ __forceinline__ void dma4s(uint32_t voff, const void* sbase, uint32_t lds) {
+    sbase = sgpr_ptr(sbase);
+    lds = __builtin_amdgcn_readfirstlane(lds);
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sbase), "s"(lds)
+                 : "memory", "m0");
+}
+// wait until at most n (wave-uniform, <= 15) vector-memory ops of this wave are in
+// flight, then barrier: vmcnt retires in issue order for loads (the DMAs)
+__device__ __forceinline__ void wait_dma_barrier(int n) {
+#define KNN_WAIT_CASE(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")\n\ts_barrier" ::: "memory"); break;
+    switch (n) {
+        KNN_WAIT_CASE(1) KNN_WAIT_CASE(2) KNN_WAIT_CASE(3) KNN_WAIT_CASE(4) KNN_WAIT_CASE(5)
+        KNN_WAIT_CASE(6) KNN_WAIT_CASE(7) KNN_WAIT_CASE(8) KNN_WAIT_CASE(9) KNN_WAIT_CASE(10)
+        KNN_WAIT_CASE(11) KNN_WAIT_CASE(12) KNN_WAIT_CASE(13) KNN_WAIT_CASE(14) KNN_WAIT_CASE(15)
+        default: asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    }
+#undef KNN_WAIT_CASE
+}
+
+// per-query 4-ary heap stride in floats: node n >= 1 in slot n-1, the root in the last slot;
+// slots of nodes >= k hold -inf up to the last child group a parent < k reads (slot k+1)
+__host__ __device__ __forceinline__ int heap_stride(int k) { return (k + 3 + 3) & ~3; }
+
+// tile geometry shared by the kernel and the host's LDS sizing: NW waves per block,
+// QG 32-query groups per wave, RG 32-row groups per tile; NACC = QG * RG accumulators
+template <int RB, int NW, int QG, int RG>
+struct FilterTile {
+    static constexpr int NACC = QG * RG;             // 32x32 accumulators per wave per tile
+    static constexpr int BN = 32 * RG;               // train rows per tile
+    static constexpr int BM = 32 * QG * NW;          // queries per block
+    static constexpr int STRIDE = RB + 16;           // LDS bytes per tile row
+    static constexpr int SLOTS = RB / 16 + 1;        // 16-B slots per padded row
+    static constexpr int DMA_INS = (BN * SLOTS + 63) / 64;     // 1 KiB DMA instructions per tile
+    static constexpr int LAST_LANES = BN * SLOTS - 64 * (DMA_INS - 1);  // active lanes of the last
+    static constexpr int TILE = DMA_INS * 1024;      // LDS bytes per buffer (>= BN * STRIDE)
+};

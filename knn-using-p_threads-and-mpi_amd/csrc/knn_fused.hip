@@ -1,0 +1,611 @@
+// knn_fused.hip -- the GEMM-form candidate filter on the bf16 MFMA with the train norm
+// folded into the MFMA (gfx950).  DESIGN.md "Fused-norm filter".
+//
+// Rows are augmented by 16 bf16 columns (k_aug_rows):
+//   train  [ rn(t_0) .. rn(t_{d-1}) | tn_hi tn_mid tn_lo 0 x 13 ]   (tn = ||t||^2, fp32)
+//   query  [ -2 rn(q_0) .. -2 rn(q_{d-1}) | 1 1 1 0 x 13 ]
+// so one chain of v_mfma_f32_32x32x16_bf16 over d/16 + 1 k-steps leaves
+//   y = tn - 2 rn(q).rn(t)
+// in the accumulators: the fast test is a v_min3 chain over the 16 values of an
+// accumulator against one per-(query, tile) threshold, with no per-value norm read or
+// fma; the slow path walks the values in a runtime loop with a wave-uniform index (a
+// scalar-indexed register read, no scratch), computes the exact certificate bounds
+//   G = qn + y,  Delta = coef (qn + tn) + eta,  L = G - Delta <= D <= U = G + Delta
+// (D: the reference's direct-form distance, main.cpp:14-23) and keeps (row, L, U) for
+// the exact rescore (k_rescore) exactly like k_gemm_filter.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "knn_device.h"
+#include "knn_kernels.h"
+#include "knn_study.h"
+
+#ifndef KNN_FUSED_PF
+#define KNN_FUSED_PF 6  // A-fragment prefetch depth in MFMAs
+#endif
+#ifndef KNN_FUSED_DEFER
+#define KNN_FUSED_DEFER 1  // 8-wave shapes: queue passing values, flush all waves together
+#endif
+#ifndef KNN_FUSED_DEFER_EVERY
+#define KNN_FUSED_DEFER_EVERY 64  // tiles between flushes of the deferred queues
+#endif
+#ifndef KNN_FUSED_RQ
+#define KNN_FUSED_RQ 4  // deferred-queue depth per lane
+#endif
+
+// ---------------------------------------------------------------------------------
+// k_aug_rows<E>: rows of the fused filter, [n][d + 16] bf16.  Element c < d is
+// rn(scale * x[r][c]) (scale = 1: train, -2: queries; exact scaling by a power of two);
+// the augmented block is the three-term bf16 split of norms[r] (train: tn = hi + mid +
+// lo + r, |r| <= 2^-24 tn, each subtraction exact by Sterbenz) or (1, 1, 1) (queries,
+// norms == NULL), then zeros.  One thread per 4 elements: a float4 (or 4 bf16) in, one
+// 8-byte bf16 quad out.
+// ---------------------------------------------------------------------------------
+template <typename E>
+__global__ __launch_bounds__(256) void k_aug_rows(const E* __restrict__ x, int64_t n, int ld, int d,
+                                                  const float* __restrict__ norms, float scale,
+                                                  bf16_t* __restrict__ out) {
+    const int per_row = (d + 16) >> 2;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n * per_row) return;
+    const int64_t r = i / per_row;
+    const int c = (int)(i - r * per_row) * 4;
+    uint32_t w0 = 0u, w1 = 0u;
+    if (c < d) {
+        const float4 v = load4(x + r * ld + c);
+        w0 = bf16_rne(scale * v.x) | (bf16_rne(scale * v.y) << 16);
+        w1 = bf16_rne(scale * v.z) | (bf16_rne(scale * v.w) << 16);
+    } else if (c == d) {
+        if (norms) {
+            const float t = norms[r];
+            const uint32_t hi = bf16_rne(t);
+            const float r1 = t - __uint_as_float(hi << 16);
+            const uint32_t mid = bf16_rne(r1);
+            const uint32_t lo = bf16_rne(r1 - __uint_as_float(mid << 16));
+            w0 = hi | (mid << 16);
+            w1 = lo;
+        } else {
+            w0 = 0x3f803f80u;  // bf16 1.0, 1.0
+            w1 = 0x00003f80u;  // 1.0, 0
+        }
+    }
+    *reinterpret_cast<uint2*>(out + r * (int64_t)(d + 16) + c) = make_uint2(w0, w1);
+}
+
+hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int ld, int d, const float* norms, float scale,
+                               uint16_t* out, hipStream_t st) {
+    const int64_t total = n * ((d + 16) / 4);
+    if (total <= 0) return hipSuccess;
+    if (d % 4 || ld % 4) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)((total + 255) / 256));
+    if (elem == ELEM_BF16)
+        hipLaunchKernelGGL(k_aug_rows<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, n, ld, d, norms, scale,
+                           (bf16_t*)out);
+    else
+        hipLaunchKernelGGL(k_aug_rows<float>, grid, dim3(256), 0, st, (const float*)x, n, ld, d, norms, scale,
+                           (bf16_t*)out);
+    KNN_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------------
+// k_gemm_fused<RB, MINW, NBUF, NW, RG>: the filter (RB = bytes per augmented row,
+// 2d + 32).  Block = NW waves x 32 queries; a train tile has BN = 32 RG rows, copied
+// global -> LDS by LDS-DMA (NBUF buffers, one barrier per tile, pieces issued between
+// the MFMAs) with each row padded to RB + 16 bytes (conflict-free ds_read_b128 of the A
+// fragments).  Lane (j, h) holds 16 bytes of its query's augmented row per k-step in
+// VGPRs (the B fragment) for the whole scan; register r of accumulator c holds train
+// row 32c + (r & 3) + 8 (r >> 2) + 4h of the tile against query j.  Per tile each wave
+// issues the MFMAs of tile it into X while the fast test of tile it-1 (Y) runs in
+// between (software pipelining).
+//
+// Fast test: the tile passes for query q when min_r y_r <= tf(q, tile), with
+//   tf = (thr - qn) + coef qn + eta + 2^-18 (|thr| + qn) + (coef + 2^-18) tmax_tile,
+// tmax_tile >= tn of every row of the tile (k_row_norms' per-64-row maxima): a superset
+// of the exact test L <= thr (2^-18 (...) covers the few fp32 roundings between the two
+// forms, <= 2^-21 of the same magnitudes).
+// Threshold thr: the k-th smallest U among rows this block kept (per-query 4-ary
+// max-heap in LDS, as k_gemm_filter), or a smaller bound published by another segment
+// (gthr).  Every row of the exact top-k has L <= D <= D_(k) <= thr, so it is kept.
+// ---------------------------------------------------------------------------------
+template <int RB, int MINW, int NBUF, int NW, int RG>
+__global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) {
+    typedef FilterTile<RB, NW, 1, RG> FT;
+    constexpr int NACC = RG, BN = FT::BN, BM = FT::BM, STRIDE = FT::STRIDE, SLOTS = FT::SLOTS;
+    constexpr int DMA_INS = FT::DMA_INS, TILE = FT::TILE;
+    constexpr int NT = 64 * NW;
+    constexpr int DMA_PER_WAVE = (DMA_INS + NW - 1) / NW;
+    constexpr int NS = RB / 32;                  // k-steps: d/16 feature steps + the norm step
+    constexpr int NR = NBUF + 1;                 // norm ring slots
+    constexpr int VPS = (16 + NS - 1) / NS;      // fast-test values folded per k-step per accumulator
+    static_assert(NBUF == 2 || NBUF == 3, "tile buffers");
+    static_assert(RG == 1 || RG == 2, "row groups");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char* tiles = smem;                                     // [NBUF][TILE]
+    float* ring = reinterpret_cast<float*>(smem + NBUF * TILE);      // [NR][BN] train norms tn
+    const int hs = heap_stride(a.k);
+    float* topU = ring + NR * BN;                                    // [BM][hs] max-heaps of U
+    const int cap_sub = a.cap_seg / 2;  // candidate sub-slice of one lane half (h) of a query
+
+    const int lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int j = lane & 31;
+    const int h = lane >> 5;
+    const int qt = blockIdx.x % a.n_qtiles;
+    const int seg = blockIdx.x / a.n_qtiles;
+    const int64_t row_begin = (int64_t)seg * a.seg_len;
+    const int64_t row_end = min(a.nt, row_begin + a.seg_len);
+    const int k = a.k;
+    const float INF = __uint_as_float(0x7f800000u);
+    const float coef = a.coef, eta = a.eta;
+    const int64_t ldb = (int64_t)a.ld_t * 2;  // augmented train row pitch, bytes
+    const unsigned char* trainb = reinterpret_cast<const unsigned char*>(a.train);
+
+    for (int i = threadIdx.x; i < BM * hs; i += NT) {
+        const int e = i % hs;
+        topU[i] = (e == hs - 1 || e <= k - 2) ? INF : -INF;  // root, nodes 1..k-1: +inf
+    }
+    for (int i = threadIdx.x; i < NR * BN; i += NT) ring[i] = INF;
+
+    // this lane's query (both lane halves hold the same query, different rows)
+    const int jl = wave * 32 + j;
+    const int64_t q = (int64_t)qt * BM + jl;
+    const bool qvalid = q < a.nq;
+    uint4 qf[NS];
+    {
+        const unsigned char* qrow = reinterpret_cast<const unsigned char*>(a.test) +
+                                    (qvalid ? q : 0) * (int64_t)a.ld_q * 2;
+#pragma unroll
+        for (int s = 0; s < NS; s++)
+            qf[s] = qvalid ? *reinterpret_cast<const uint4*>(qrow + 32 * s + 16 * h) : make_uint4(0u, 0u, 0u, 0u);
+    }
+    const float qn = qvalid ? a.qnorm[q] : 0.0f;
+    float thr = qvalid ? o2f(a.gthr[q]) : -INF;
+    float published = thr;
+    float root = INF;  // this query's heap root, mirrored in both lanes
+    int ccnt = 0;      // candidates this lane half kept
+    float tfb;         // tf without the tile term
+    auto make_tfb = [&]() __attribute__((always_inline)) {
+        tfb = qvalid ? ((thr - qn) + fmaf(coef, qn, eta)) + 0x1p-18f * (fabsf(thr) + qn) : -INF;
+    };
+    make_tfb();
+    auto tf_of = [&](float tm) __attribute__((always_inline)) { return fmaf(coef + 0x1p-18f, tm, tfb); };
+
+    // ---- LDS-DMA of tiles (same image as k_gemm_filter: slot P -> row P / SLOTS, slot P % SLOTS,
+    // the pad slot duplicates slot 0; rows past nt read row nt-1 and are rejected by index)
+    uint32_t doff[DMA_PER_WAVE];
+#pragma unroll
+    for (int i = 0; i < DMA_PER_WAVE; i++) {
+        const int P = (wave + NW * i) * 64 + lane;
+        const int row = min(P / SLOTS, BN - 1), sl = P % SLOTS;
+        doff[i] = (uint32_t)(row * ldb + 16 * (sl == SLOTS - 1 ? 0 : sl));
+    }
+    int n_dma_wave = (wave == NW - 1) ? 1 : 0;  // + the norm ring load
+#pragma unroll
+    for (int i = 0; i < DMA_PER_WAVE; i++) n_dma_wave += (wave + NW * i < DMA_INS) ? 1 : 0;
+    constexpr int NPIECE = DMA_PER_WAVE + 1;
+    const uint32_t lds_tiles = __builtin_amdgcn_readfirstlane(lds_addr(tiles));
+    const uint32_t lds_ring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+    struct DmaTile { const unsigned char* src; uint32_t lds, lring; int64_t r0; bool full; };
+    auto dma_desc = [&](int buf, int slot, int64_t r0) -> DmaTile {
+        return DmaTile{trainb + r0 * ldb, lds_tiles + (uint32_t)(buf * TILE), lds_ring + (uint32_t)(slot * BN * 4), r0,
+                       r0 + BN <= a.nt};
+    };
+    auto dma_piece = [&](int i, const DmaTile& d) __attribute__((always_inline)) {
+        if (i < DMA_PER_WAVE) {
+            const int ins = wave + NW * i;
+            if (ins < DMA_INS) {
+                if (i == DMA_PER_WAVE - 1 && ins == DMA_INS - 1 && lane >= FT::LAST_LANES) return;
+                const uint32_t dst = d.lds + (uint32_t)ins * 1024u;
+                if (d.full) {
+                    dma16s(doff[i], d.src, dst);
+                } else {
+                    const int P = ins * 64 + lane;
+                    const int row = P / SLOTS, sl = P % SLOTS;
+                    const int64_t t = min(d.r0 + row, a.nt - 1);
+                    dma16(trainb + t * ldb + 16 * (sl == SLOTS - 1 ? 0 : sl), dst);
+                }
+            }
+        } else if (wave == NW - 1 && lane < BN) {
+            dma4s(4u * lane, a.tnorm + d.r0, d.lring);
+        }
+    };
+    auto dma_tile = [&](int buf, int slot, int64_t r0) __attribute__((always_inline)) {
+        const DmaTile d = dma_desc(buf, slot, r0);
+#pragma unroll
+        for (int i = 0; i < NPIECE; i++) dma_piece(i, d);
+    };
+    auto dma_at = [&](int s, bool on, const DmaTile& d) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < NPIECE; i++)
+            if (on && (i * NS) / NPIECE == s) dma_piece(i, d);
+    };
+
+    // ---- one tile's MFMAs into X, the fast-test minimum of the previous tile (Y) in between
+    auto step = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int buf, bool dma_on, const DmaTile& dd) -> float {
+        const unsigned char* tile = tiles + buf * TILE;
+        const unsigned char* a0p = tile + j * STRIDE + 16 * h;
+        const unsigned char* a1p = tile + ((RG == 2 ? 32 : 0) + j) * STRIDE + 16 * h;
+#pragma unroll
+        for (int c = 0; c < NACC; c++) X[c] = floatx16{};
+        float mn[NACC];
+#pragma unroll
+        for (int c = 0; c < NACC; c++) mn[c] = INF;
+        constexpr int PF = KNN_FUSED_PF / NACC;
+        uint4 xa[NS], xb[NS];
+#pragma unroll
+        for (int s = 0; s < PF && s < NS; s++) {
+            xa[s] = *reinterpret_cast<const uint4*>(a0p + 32 * s);
+            if (RG == 2) xb[s] = *reinterpret_cast<const uint4*>(a1p + 32 * s);
+        }
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+            dma_at(s, dma_on, dd);
+            if (s + PF < NS) {
+                xa[s + PF] = *reinterpret_cast<const uint4*>(a0p + 32 * (s + PF));
+                if (RG == 2) xb[s + PF] = *reinterpret_cast<const uint4*>(a1p + 32 * (s + PF));
+            }
+#pragma unroll
+            for (int c = 0; c < NACC; c++) {
+                const bf16x8 A = __builtin_bit_cast(bf16x8, (RG == 2 && c) ? xb[s] : xa[s]);
+                X[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, __builtin_bit_cast(bf16x8, qf[s]), X[c], 0, 0, 0);
+#ifndef KNN_ABLATE_NO_EPI
+#pragma unroll
+                for (int v = s * VPS; v < (s + 1) * VPS && v < 16; v++) mn[c] = fminf(mn[c], Y[c][v]);
+#endif
+            }
+            __builtin_amdgcn_sched_barrier(0);  // keep this k-step's order (prefetch, MFMA, VALU)
+        }
+        float m = mn[0];
+#pragma unroll
+        for (int c = 1; c < NACC; c++) m = fminf(m, mn[c]);
+        return m;
+    };
+
+#ifdef KNN_FILTER_TIMING
+    unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define KNN_TSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define KNN_TSTAMP(v)
+#endif
+
+    // keep candidate (L, U) of global row t: the exact test against the current threshold,
+    // the candidate store into this lane half's sub-slice, and, if U beats the heap root, a
+    // sift-down of the query's 4-ary max-heap (node n >= 1 in H[n-1], the root in H[hs-1]:
+    // the four children of node i are one aligned 16-byte read at H[4i]).  Only one lane of
+    // a query runs it at a time.
+    auto accept = [&](float L, float U, int64_t t) __attribute__((always_inline)) {
+        if (!(L <= thr)) return;
+        if (ccnt < cap_sub) {
+            const int64_t o = q * (int64_t)a.cap + (int64_t)(2 * seg + h) * cap_sub + ccnt;
+            a.cand_idx[o] = (int32_t)t;
+            a.cand_L[o] = L;
+            a.cand_U[o] = U;
+        }
+        ccnt++;
+        if (U < root) {
+            float* H = topU + jl * hs;
+            int i = 0;
+            float newroot = U;
+            for (;;) {
+                if (4 * i + 1 > k - 1) break;
+                const float4 cc = *reinterpret_cast<const float4*>(H + 4 * i);
+                const float cm = fmaxf(fmaxf(cc.x, cc.y), fmaxf(cc.z, cc.w));
+                if (cm <= U) break;
+                const int ci = cm == cc.x ? 0 : cm == cc.y ? 1 : cm == cc.z ? 2 : 3;
+                H[i == 0 ? hs - 1 : i - 1] = cm;
+                if (i == 0) newroot = cm;
+                i = 4 * i + 1 + ci;
+            }
+            H[i == 0 ? hs - 1 : i - 1] = U;
+            root = newroot;
+            thr = fminf(thr, root);
+        }
+    };
+    auto sync_roots = [&](int hh) __attribute__((always_inline)) {
+        const float other = __shfl_xor(root, 32);
+        if (h != hh) root = other;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    };
+    auto publish = [&]() __attribute__((always_inline)) {
+        if (qvalid) {
+            thr = fminf(thr, root);
+            if (a.nseg > 1 && h == 0 && thr < published) {
+                atomicMin(&a.gthr[q], f2o(thr));
+                published = thr;
+            }
+            make_tfb();
+        }
+    };
+    // exact bounds of value r of accumulator c of tile tp (row `row`)
+    auto bounds = [&](float y, int row, int tp, float& L, float& U) __attribute__((always_inline)) {
+        const float G = qn + y;
+        const float dl = fmaf(coef, qn + ring[(tp % NR) * BN + row], eta);
+        L = G - dl;
+        U = G + dl;
+    };
+
+    // value v (wave-uniform) of accumulators Y: a scalar-indexed register read (v_movrels),
+    // so the walk below is a runtime loop with one copy of its body -- a static walk over
+    // the 16 NACC values replicates accept() per value, and the code no longer fits the
+    // instruction cache (measured 10x slower on B)
+    auto yval = [&](floatx16 (&Y)[NACC], int v) __attribute__((always_inline)) -> float {
+        if constexpr (NACC == 1) return Y[0][v & 15];
+        else return (v >> 4) ? Y[1][v & 15] : Y[0][v & 15];
+    };
+    // the values of Y some lane passes: bit v set iff value v passes in any lane (one
+    // v_cmp per value into an SGPR pair, then scalar ops)
+    auto pass_set = [&](floatx16 (&Y)[NACC], float tf) __attribute__((always_inline)) -> uint32_t {
+        uint32_t u = 0u;
+#pragma unroll
+        for (int c = 0; c < NACC; c++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) u |= (__ballot(Y[c][r] <= tf) != 0ull ? 1u : 0u) << (16 * c + r);
+        return u;
+    };
+    // immediate slow path: the passing values of tile tp, visited by index; the two lanes
+    // of a query take turns (one heap writer at a time)
+    auto slow = [&](floatx16 (&Y)[NACC], int tp, float tf) {
+        const int64_t tbase = row_begin + (int64_t)tp * BN;
+        uint32_t u = pass_set(Y, tf);
+        while (u) {
+            const int v = __builtin_ctz(u);
+            u &= u - 1u;
+            const float y = yval(Y, v);
+            const bool p = y <= tf;
+            const int r = v & 15;
+            const int row = 32 * (v >> 4) + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int64_t t = tbase + row;
+#pragma unroll 1
+            for (int hh = 0; hh < 2; hh++) {
+                if (!__ballot(p && h == hh)) continue;
+                if (p && h == hh && t < row_end) {
+                    float L, U;
+                    bounds(y, row, tp, L, U);
+                    accept(L, U, t);
+                }
+                sync_roots(hh);
+            }
+        }
+        publish();
+    };
+
+    // deferred slow path (8-wave shapes): passing values with L <= thr are queued -- (L, U,
+    // row) in registers -- and flushed through accept() every DEFER_EVERY tiles by all waves
+    // together, or when some lane's queue is full.  A threshold waiting for the flush is
+    // stale but still valid (it only ever tightens).
+    // the queue is three register vectors read with a wave-uniform index (v_movrels), so
+    // the flush is a runtime loop with one copy of accept()
+    constexpr int RQ = KNN_FUSED_RQ;
+    static_assert(RQ == 2 || RQ == 4 || RQ == 8, "queue depth");
+    typedef float qvecf __attribute__((ext_vector_type(RQ)));
+    typedef int qveci __attribute__((ext_vector_type(RQ)));
+    qvecf qL = qvecf{}, qU = qvecf{};
+    qveci qT = qveci{};
+    int qcnt = 0;
+    auto flush = [&]() __attribute__((always_inline)) {
+#ifdef KNN_FILTER_TIMING
+        const unsigned long long tf0 = __builtin_amdgcn_s_memtime();
+#endif
+#pragma unroll 1
+        for (int hh = 0; hh < 2; hh++) {
+#pragma unroll 1
+            for (int i = 0; i < RQ; i++) {
+                const bool mine = h == hh && i < qcnt;
+                if (!__ballot(mine)) break;
+                if (mine) accept(qL[i], qU[i], (int64_t)qT[i]);
+            }
+            sync_roots(hh);
+        }
+        qcnt = 0;
+        publish();
+#ifdef KNN_FILTER_TIMING
+        tph[6] += 1;
+        tph[7] += __builtin_amdgcn_s_memtime() - tf0;
+#endif
+    };
+    auto record = [&](floatx16 (&Y)[NACC], int tp, float tf) {
+        const int64_t tbase = row_begin + (int64_t)tp * BN;
+        uint32_t u = pass_set(Y, tf);
+#ifdef KNN_FILTER_TIMING
+        tph[4] += 1;
+        tph[5] += __builtin_popcount(u);
+#endif
+        while (u) {
+            const int v = __builtin_ctz(u);
+            u &= u - 1u;
+            const float y = yval(Y, v);
+            const bool p = y <= tf;
+            if (__ballot(p && qcnt >= RQ)) flush();
+            const int r = v & 15;
+            const int row = 32 * (v >> 4) + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int64_t t = tbase + row;
+            if (p && t < row_end) {
+                float L, U;
+                bounds(y, row, tp, L, U);
+                if (L <= thr) {
+#pragma unroll
+                    for (int i = 0; i < RQ; i++) {
+                        qL[i] = i == qcnt ? L : qL[i];
+                        qU[i] = i == qcnt ? U : qU[i];
+                        qT[i] = i == qcnt ? (int)t : qT[i];
+                    }
+                    qcnt++;
+                }
+            }
+        }
+    };
+
+    const int ntiles = (row_end > row_begin) ? (int)((row_end - row_begin + BN - 1) / BN) : 0;
+    floatx16 accA[NACC], accB[NACC];
+#pragma unroll
+    for (int c = 0; c < NACC; c++) accA[c] = accB[c] = floatx16{};
+    __syncthreads();  // LDS init is complete before any DMA lands
+#pragma unroll
+    for (int p = 0; p < NBUF - 1; p++)
+        if (p < ntiles) dma_tile(p, p, row_begin + (int64_t)p * BN);
+#ifndef KNN_FUSED_EARLY_DMA
+#define KNN_FUSED_EARLY_DMA 0
+#endif
+    constexpr bool LATE_DMA = NBUF == 3 && !KNN_FUSED_EARLY_DMA;
+    constexpr bool DEFER = NW == 8 && KNN_FUSED_DEFER;
+    constexpr int DEFER_EVERY = KNN_FUSED_DEFER_EVERY;
+    bool dirty = false;  // this wave issued vector-memory ops after the newest DMA
+    // per-64-row maximum train norm of the tile in the pipeline (tile it) and of tile it-1
+    const float* tmaxp = a.tmax + (row_begin >> 6);
+    float tm_prev = 0.0f;
+    auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
+        const int64_t r0 = row_begin + (int64_t)it * BN;
+        if ((it & 63) == 63 && a.nseg > 1 && qvalid) {
+            // thresholds published by other segments of this query
+            const float gv = o2f(__hip_atomic_load(&a.gthr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (gv < thr) { thr = gv; make_tfb(); }
+        }
+        const bool keep_next = NBUF == 3 && it + 1 < ntiles && (LATE_DMA || !dirty);
+        KNN_TSTAMP(t0);
+        wait_dma_barrier(keep_next ? n_dma_wave : 0);
+        dirty = false;
+        // this tile's maximum train norm, for its fast test in the next iteration: issued after
+        // the barrier, it lands under this step (the next barrier's wait covers it)
+        const float tm_cur = tmaxp[(it * BN) >> 6];
+        KNN_TSTAMP(t1);
+#ifndef KNN_ABLATE_NO_DMA
+        const bool dma_on = it + NBUF - 1 < ntiles;
+#else
+        const bool dma_on = false;
+#endif
+        const DmaTile dd = dma_desc((it + NBUF - 1) % NBUF, (it + NBUF - 1) % NR, r0 + (int64_t)(NBUF - 1) * BN);
+        const float mnY = step(X, Y, it % NBUF, dma_on && !LATE_DMA, dd);
+        KNN_TSTAMP(t2);
+#ifndef KNN_ABLATE_NO_SLOW
+        if (it > 0) {
+            const float tf = tf_of(tm_prev);
+            if (__ballot(mnY <= tf)) {
+                if constexpr (DEFER) record(Y, it - 1, tf);
+                else { slow(Y, it - 1, tf); dirty = true; }
+            }
+        }
+        if constexpr (DEFER) {
+            if ((it & (DEFER_EVERY - 1)) == DEFER_EVERY - 1 && __ballot(qcnt > 0)) {
+                flush();
+                dirty = true;
+            }
+        }
+#else
+        asm volatile("" ::"v"(mnY));
+#endif
+        if (LATE_DMA && dma_on) {
+#pragma unroll
+            for (int i = 0; i < NPIECE; i++) dma_piece(i, dd);
+        }
+        tm_prev = tm_cur;
+#ifdef KNN_FILTER_TIMING
+        KNN_TSTAMP(t3);
+        tph[0] += t1 - t0; tph[2] += t2 - t1; tph[3] += t3 - t2;
+#endif
+    };
+    for (int it = 0; it < ntiles; it += 2) {
+        iter(accA, accB, it);
+        if (it + 1 < ntiles) iter(accB, accA, it + 1);
+    }
+    if (ntiles > 0) {
+        // drain: the last tile's accumulators are in accA (ntiles odd) or accB (even)
+        const int last = ntiles - 1;
+        auto drain = [&](floatx16 (&Lc)[NACC]) {
+            float m = INF;
+#pragma unroll
+            for (int c = 0; c < NACC; c++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) m = fminf(m, Lc[c][r]);
+            const float tf = tf_of(tm_prev);
+            if (__ballot(m <= tf)) {
+                if constexpr (DEFER) record(Lc, last, tf);
+                else slow(Lc, last, tf);
+            }
+        };
+        if (last & 1) drain(accB);
+        else drain(accA);
+    }
+    if constexpr (DEFER) {
+        if (__ballot(qcnt > 0)) flush();
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (qvalid) a.cnt[(int64_t)(2 * seg + h) * a.nq + q] = ccnt;
+#ifdef KNN_FILTER_TIMING
+    if (a.timing && lane == 0) {
+        atomicAdd(&a.timing[0], tph[0]);
+        atomicAdd(&a.timing[2], tph[2]);
+        atomicAdd(&a.timing[3], tph[3]);
+        atomicAdd(&a.timing[4], 1ull);
+        atomicAdd(&a.timing[6], tph[4]);  // record calls
+        atomicAdd(&a.timing[7], tph[5]);  // passing value indices visited
+        atomicAdd(&a.timing[8], tph[6]);  // flushes
+        atomicAdd(&a.timing[5], tph[7]);  // flush clocks
+    }
+#endif
+#undef KNN_TSTAMP
+}
+
+// ---------------------------------------------------------------------------------
+// plan and launch
+// ---------------------------------------------------------------------------------
+static size_t fused_lds_of(int row_bytes, int k, int nw, int rg, int nbuf) {
+    const int bn = 32 * rg, bm = 32 * nw;
+    const int ins = (bn * (row_bytes / 16 + 1) + 63) / 64;
+    return (size_t)nbuf * ins * 1024 + ((size_t)(nbuf + 1) * bn + (size_t)bm * heap_stride(k)) * sizeof(float);
+}
+
+bool knn_fused_supported(int d) { return d == 64 || d == 128 || d == 256; }
+
+// Shapes (d = features; rows of 2d + 32 bytes):
+//  d = 64:   4 waves x 32 queries, 64-row tiles, two blocks per CU (short rows: the per-tile
+//            barrier and fast test outweigh 5 MFMAs per 32x32 block; the other block hides them)
+//  d >= 128: 8 waves x 32 queries (two waves per SIMD), 64-row tiles, double-buffered; 32-row
+//            tiles when the per-query heaps of a large k leave no room for 64-row tiles.
+FilterPlan knn_fused_plan(int d, int k, const FilterStudy* fs) {
+    const int rb = 2 * d + 32;
+    const size_t cap = 160 * 1024;
+    auto make = [&](int nw, int rg, int minw, int nbuf) {
+        return FilterPlan{nw, 1, rg, minw, nbuf, 32 * nw, fused_lds_of(rb, k, nw, rg, nbuf)};
+    };
+    const bool force8 = fs && fs->shape[0] == 'w' && fs->shape[1] == '8';
+    const int nb = fs && fs->nbuf == 3 ? 3 : 2;  // kernel study: triple-buffered tiles
+    if (d == 64 && !force8 && fused_lds_of(rb, k, 4, 2, nb) <= cap / 2) return make(4, 2, 2, nb);
+    if (fused_lds_of(rb, k, 8, 2, nb) <= cap) return make(8, 2, 2, nb);
+    if (fused_lds_of(rb, k, 8, 1, 2) <= cap) return make(8, 1, 2, 2);
+    return FilterPlan{0, 0, 0, 0, 0, 0, 0};  // k too large for the LDS heaps: not supported
+}
+
+template <int RB>
+static const void* fused_fn(const FilterPlan& f) {
+    if (f.nw == 4) return f.nbuf == 3 ? reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, 3, 4, 2>)
+                                      : reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, 2, 4, 2>);
+    if (f.rg == 2) return f.nbuf == 3 ? reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, 3, 8, 2>)
+                                      : reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, 2, 8, 2>);
+    return reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, 2, 8, 1>);
+}
+
+static const void* fused_ptr(int d, const FilterPlan& f) {
+    return d == 64 ? fused_fn<160>(f) : d == 128 ? fused_fn<288>(f) : fused_fn<544>(f);
+}
+
+hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu, const FilterStudy* fs) {
+    const FilterPlan f = knn_fused_plan(d, k, fs);
+    if (!knn_fused_supported(d) || f.nw == 0) return hipErrorInvalidValue;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fused_ptr(d, f), 64 * f.nw, f.lds);
+}
+
+hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st, const FilterStudy* fs) {
+    const FilterPlan f = knn_fused_plan(a.d, a.k, fs);
+    if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != a.d + 16 || a.ld_q != a.d + 16 || !a.tmax)
+        return hipErrorInvalidValue;
+    void* args[] = {const_cast<GemmFilterArgs*>(&a)};
+    const dim3 grid((unsigned)(a.n_qtiles * a.nseg));
+    hipError_t e = hipLaunchKernel(fused_ptr(a.d, f), grid, dim3(64 * f.nw), args, f.lds, st);
+    if (e != hipSuccess) return e;
+    KNN_LAUNCH_CHECK();
+    return hipSuccess;
+}

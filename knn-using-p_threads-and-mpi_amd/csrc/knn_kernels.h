@@ -49,6 +49,7 @@ struct GemmFilterArgs {
     unsigned long long* timing;  // KNN_FILTER_TIMING builds: per-phase shader clocks (else NULL)
     int32_t* cnt;  // [nseg][nq] kept rows per (segment, query)
     int32_t* cand_idx; float* cand_L; float* cand_U; int cap; int cap_seg;
+    const float* tmax;  // fused filter: per-64-row maximum train norm
 };
 
 struct RescoreArgs {
@@ -109,8 +110,10 @@ struct GenerateArgs {
 
 hipError_t knn_launch_exact_scan(const ExactScanArgs& a, int grid, hipStream_t st);
 size_t knn_exact_scan_lds(int d, int k, int C);
+// tmax (optional): the maximum norm of every 64-row tile, [ceil(n / 64)] (the fused filter)
 hipError_t knn_launch_row_norms(const void* x, int elem, int64_t n, int ld, int d, float* out,
-                                int32_t* status, uint32_t* maxo, float* outp, float c1, hipStream_t st);
+                                int32_t* status, uint32_t* maxo, float* outp, float c1, hipStream_t st,
+                                float* tmax = nullptr);
 // row_bytes = d * element size: 128, 256 or 512
 bool knn_gemm_filter_supported(int elem, int row_bytes);
 // block shape of the filter for (element type, row bytes, k): waves per block, query
@@ -130,6 +133,14 @@ hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks
 hipError_t knn_launch_split_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st);
 hipError_t knn_launch_round_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st);
 hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st);
+// fused-norm filter (knn_fused.hip): rows augmented to d + 16 bf16 (k_aug_rows), d in {64, 128, 256}
+bool knn_fused_supported(int d);
+FilterPlan knn_fused_plan(int d, int k, const FilterStudy* fs = nullptr);  // nw == 0: k too large
+hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu, const FilterStudy* fs = nullptr);
+hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st, const FilterStudy* fs = nullptr);
+// x [n][ld] (fp32 or bf16) -> bf16 [n][d + 16]: rn(scale * x) | split of norms[r] (or 1 1 1) | 0
+hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int ld, int d, const float* norms, float scale,
+                               uint16_t* out, hipStream_t st);
 // Starting thresholds of the GEMM filter (k_seed_threshold): gthr[q] = ordered k-th
 // smallest exact D from query q to ns <= KNN_SEED_MAX_ROWS rows spread over train.
 #define KNN_SEED_MAX_ROWS 2048
@@ -142,5 +153,7 @@ struct SeedArgs {
 hipError_t knn_launch_seed_threshold(const SeedArgs& a, int elem, hipStream_t st);
 hipError_t knn_launch_merge(const MergeArgs& a, hipStream_t st);
 hipError_t knn_launch_generate(const GenerateArgs& a, hipStream_t st);
+// the bf16 filter's MFMA chain on [32][K] bf16 operands (certificate self-test)
+hipError_t knn_launch_mfma_probe(const uint16_t* a, const uint16_t* b, int K, float* out, hipStream_t st);
 hipError_t knn_launch_confusion(const int32_t* pred, const int32_t* labels, int64_t n, int C, int32_t* cm,
                                 unsigned long long* correct, int32_t* status, hipStream_t st);
