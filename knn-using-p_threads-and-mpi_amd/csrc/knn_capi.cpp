@@ -64,7 +64,7 @@ struct knn_ctx {
     DBuf tmax;              // fused filter: per-64-row maximum train norm
     // kernel-study switches, read once from the environment in knn_create (never in a call)
     int study_seed = 0, study_timing = 0, study_nofused = 0;
-    FilterStudy fstudy{0, {0}};
+    FilterStudy fstudy{0, {0}, -1};
     // host-API staging (device copies of host inputs / outputs)
     DBuf h_train, h_labels, h_test, h_pred, h_dist, h_idx;
     int32_t* ctrl_host = nullptr;  // pinned: [0] status, [1] fallback count
@@ -524,6 +524,7 @@ knn_status knn_create(knn_ctx** out, const knn_opts* opts) {
     if (getenv("KNN_FILTER_TIMING")) c->study_timing = 1;
     if (const char* e = getenv("KNN_FILTER_FUSED")) c->study_nofused = atoi(e) == 0;
     if (const char* e = getenv("KNN_FILTER_NBUF")) c->fstudy.nbuf = atoi(e);
+    if (const char* e = getenv("KNN_FILTER_PSTEP")) c->fstudy.pstep = atoi(e);
     if (const char* e = getenv("KNN_FILTER_SHAPE")) snprintf(c->fstudy.shape, sizeof(c->fstudy.shape), "%s", e);
     if (c->device < 0 || c->device >= ndev) { delete c; return KNN_ENODEV; }
     hipDeviceProp_t prop;

@@ -109,7 +109,7 @@ hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int ld, int d
 // max-heap in LDS, as k_gemm_filter), or a smaller bound published by another segment
 // (gthr).  Every row of the exact top-k has L <= D <= D_(k) <= thr, so it is kept.
 // ---------------------------------------------------------------------------------
-template <int RB, int MINW, int NBUF, int NW, int RG>
+template <int RB, int MINW, int NBUF, int NW, int RG, bool PSTEP>
 __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) {
     typedef FilterTile<RB, NW, 1, RG> FT;
     constexpr int NACC = RG, BN = FT::BN, BM = FT::BM, STRIDE = FT::STRIDE, SLOTS = FT::SLOTS;
@@ -117,15 +117,16 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
     constexpr int NT = 64 * NW;
     constexpr int DMA_PER_WAVE = (DMA_INS + NW - 1) / NW;
     constexpr int NS = RB / 32;                  // k-steps: d/16 feature steps + the norm step
-    constexpr int NR = NBUF + 1;                 // norm ring slots
-    constexpr int VPS = (16 + NS - 1) / NS;      // fast-test values folded per k-step per accumulator
+    constexpr int VPS = (16 + NS - 1) / NS;      // fast-test values per k-step per accumulator
+    constexpr int NR = NBUF + 1;                 // norm ring slots: tiles it-1 .. it+NBUF-1
+    constexpr int RS = BN;                       // ring slot: BN row norms
     static_assert(NBUF == 2 || NBUF == 3, "tile buffers");
     static_assert(RG == 1 || RG == 2, "row groups");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* tiles = smem;                                     // [NBUF][TILE]
-    float* ring = reinterpret_cast<float*>(smem + NBUF * TILE);      // [NR][BN] train norms tn
+    float* ring = reinterpret_cast<float*>(smem + NBUF * TILE);      // [NR][RS] train norms tn
     const int hs = heap_stride(a.k);
-    float* topU = ring + NR * BN;                                    // [BM][hs] max-heaps of U
+    float* topU = ring + NR * RS;                                    // [BM][hs] max-heaps of U
     const int cap_sub = a.cap_seg / 2;  // candidate sub-slice of one lane half (h) of a query
 
     const int lane = lane_id();
@@ -146,7 +147,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
         const int e = i % hs;
         topU[i] = (e == hs - 1 || e <= k - 2) ? INF : -INF;  // root, nodes 1..k-1: +inf
     }
-    for (int i = threadIdx.x; i < NR * BN; i += NT) ring[i] = INF;
+    for (int i = threadIdx.x; i < NR * RS; i += NT) ring[i] = INF;
 
     // this lane's query (both lane halves hold the same query, different rows)
     const int jl = wave * 32 + j;
@@ -181,7 +182,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
         const int row = min(P / SLOTS, BN - 1), sl = P % SLOTS;
         doff[i] = (uint32_t)(row * ldb + 16 * (sl == SLOTS - 1 ? 0 : sl));
     }
-    int n_dma_wave = (wave == NW - 1) ? 1 : 0;  // + the norm ring load
+    // this wave's vector-memory ops per tile: its DMA pieces (+ the norm ring load of the
+    // last wave) and the tile-max load
+    int n_dma_wave = (wave == NW - 1) ? 2 : 1;
 #pragma unroll
     for (int i = 0; i < DMA_PER_WAVE; i++) n_dma_wave += (wave + NW * i < DMA_INS) ? 1 : 0;
     constexpr int NPIECE = DMA_PER_WAVE + 1;
@@ -189,7 +192,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
     const uint32_t lds_ring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
     struct DmaTile { const unsigned char* src; uint32_t lds, lring; int64_t r0; bool full; };
     auto dma_desc = [&](int buf, int slot, int64_t r0) -> DmaTile {
-        return DmaTile{trainb + r0 * ldb, lds_tiles + (uint32_t)(buf * TILE), lds_ring + (uint32_t)(slot * BN * 4), r0,
+        return DmaTile{trainb + r0 * ldb, lds_tiles + (uint32_t)(buf * TILE), lds_ring + (uint32_t)(slot * RS * 4), r0,
                        r0 + BN <= a.nt};
     };
     auto dma_piece = [&](int i, const DmaTile& d) __attribute__((always_inline)) {
@@ -222,13 +225,18 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
             if (on && (i * NS) / NPIECE == s) dma_piece(i, d);
     };
 
-    // ---- one tile's MFMAs into X, the fast-test minimum of the previous tile (Y) in between
-    auto step = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int buf, bool dma_on, const DmaTile& dd) -> float {
+    // ---- one tile's MFMAs into X; in between, the fast test of the previous tile (Y): bit
+    // 16c + r of the returned set is 1 iff value r of accumulator c passes (y <= tf) in some
+    // lane (one v_cmp per value into an SGPR pair; the scalar ops issue beside the MFMAs --
+    // measured faster on A than a v_min3 chain plus a separate pass over the values)
+    auto step = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int buf, bool dma_on, const DmaTile& dd,
+                    float tf) -> uint32_t {
         const unsigned char* tile = tiles + buf * TILE;
         const unsigned char* a0p = tile + j * STRIDE + 16 * h;
         const unsigned char* a1p = tile + ((RG == 2 ? 32 : 0) + j) * STRIDE + 16 * h;
 #pragma unroll
         for (int c = 0; c < NACC; c++) X[c] = floatx16{};
+        uint32_t u = 0u;
         float mn[NACC];
 #pragma unroll
         for (int c = 0; c < NACC; c++) mn[c] = INF;
@@ -251,16 +259,26 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
                 const bf16x8 A = __builtin_bit_cast(bf16x8, (RG == 2 && c) ? xb[s] : xa[s]);
                 X[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, __builtin_bit_cast(bf16x8, qf[s]), X[c], 0, 0, 0);
 #ifndef KNN_ABLATE_NO_EPI
+                if constexpr (PSTEP) {
 #pragma unroll
-                for (int v = s * VPS; v < (s + 1) * VPS && v < 16; v++) mn[c] = fminf(mn[c], Y[c][v]);
+                    for (int v = s * VPS; v < (s + 1) * VPS && v < 16; v++)
+                        u |= (__ballot(Y[c][v] <= tf) != 0ull ? 1u : 0u) << (16 * c + v);
+                } else {
+#pragma unroll
+                    for (int v = s * VPS; v < (s + 1) * VPS && v < 16; v++) mn[c] = fminf(mn[c], Y[c][v]);
+                }
 #endif
             }
             __builtin_amdgcn_sched_barrier(0);  // keep this k-step's order (prefetch, MFMA, VALU)
         }
-        float m = mn[0];
+        if constexpr (!PSTEP) {
+            // only whether some value passes; the slow path builds the set itself (pass_set)
+            float m = mn[0];
 #pragma unroll
-        for (int c = 1; c < NACC; c++) m = fminf(m, mn[c]);
-        return m;
+            for (int c = 1; c < NACC; c++) m = fminf(m, mn[c]);
+            u = __ballot(m <= tf) != 0ull ? 0xffffffffu : 0u;
+        }
+        return u;
     };
 
 #ifdef KNN_FILTER_TIMING
@@ -319,10 +337,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
             make_tfb();
         }
     };
-    // exact bounds of value r of accumulator c of tile tp (row `row`)
+    // certified bounds L <= D <= U of value y of row `row` of tile tp (its norm from the ring)
     auto bounds = [&](float y, int row, int tp, float& L, float& U) __attribute__((always_inline)) {
         const float G = qn + y;
-        const float dl = fmaf(coef, qn + ring[(tp % NR) * BN + row], eta);
+        const float dl = fmaf(coef, qn + ring[(tp % NR) * RS + row], eta);
         L = G - dl;
         U = G + dl;
     };
@@ -335,8 +353,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
         if constexpr (NACC == 1) return Y[0][v & 15];
         else return (v >> 4) ? Y[1][v & 15] : Y[0][v & 15];
     };
-    // the values of Y some lane passes: bit v set iff value v passes in any lane (one
-    // v_cmp per value into an SGPR pair, then scalar ops)
+    // the values of Y some lane passes (bit 16c + r), for the !PSTEP variant: one v_cmp per
+    // value into an SGPR pair, then scalar ops (only on tiles some value passes)
     auto pass_set = [&](floatx16 (&Y)[NACC], float tf) __attribute__((always_inline)) -> uint32_t {
         uint32_t u = 0u;
 #pragma unroll
@@ -347,9 +365,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
     };
     // immediate slow path: the passing values of tile tp, visited by index; the two lanes
     // of a query take turns (one heap writer at a time)
-    auto slow = [&](floatx16 (&Y)[NACC], int tp, float tf) {
+    auto slow = [&](floatx16 (&Y)[NACC], int tp, float tf, uint32_t u) {
         const int64_t tbase = row_begin + (int64_t)tp * BN;
-        uint32_t u = pass_set(Y, tf);
+        if constexpr (!PSTEP) u = pass_set(Y, tf);
         while (u) {
             const int v = __builtin_ctz(u);
             u &= u - 1u;
@@ -378,6 +396,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
     // stale but still valid (it only ever tightens).
     // the queue is three register vectors read with a wave-uniform index (v_movrels), so
     // the flush is a runtime loop with one copy of accept()
+    bool dirty = false;  // this wave issued vector-memory ops after the newest DMA
     constexpr int RQ = KNN_FUSED_RQ;
     static_assert(RQ == 2 || RQ == 4 || RQ == 8, "queue depth");
     typedef float qvecf __attribute__((ext_vector_type(RQ)));
@@ -406,9 +425,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
         tph[7] += __builtin_amdgcn_s_memtime() - tf0;
 #endif
     };
-    auto record = [&](floatx16 (&Y)[NACC], int tp, float tf) {
+    auto record = [&](floatx16 (&Y)[NACC], int tp, float tf, uint32_t u) {
         const int64_t tbase = row_begin + (int64_t)tp * BN;
-        uint32_t u = pass_set(Y, tf);
+        if constexpr (!PSTEP) u = pass_set(Y, tf);
 #ifdef KNN_FILTER_TIMING
         tph[4] += 1;
         tph[5] += __builtin_popcount(u);
@@ -452,7 +471,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
     constexpr bool LATE_DMA = NBUF == 3 && !KNN_FUSED_EARLY_DMA;
     constexpr bool DEFER = NW == 8 && KNN_FUSED_DEFER;
     constexpr int DEFER_EVERY = KNN_FUSED_DEFER_EVERY;
-    bool dirty = false;  // this wave issued vector-memory ops after the newest DMA
     // per-64-row maximum train norm of the tile in the pipeline (tile it) and of tile it-1
     const float* tmaxp = a.tmax + (row_begin >> 6);
     float tm_prev = 0.0f;
@@ -477,15 +495,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
         const bool dma_on = false;
 #endif
         const DmaTile dd = dma_desc((it + NBUF - 1) % NBUF, (it + NBUF - 1) % NR, r0 + (int64_t)(NBUF - 1) * BN);
-        const float mnY = step(X, Y, it % NBUF, dma_on && !LATE_DMA, dd);
+        const float tf = it > 0 ? tf_of(tm_prev) : -INF;
+        const uint32_t uY = step(X, Y, it % NBUF, dma_on && !LATE_DMA, dd, tf);
         KNN_TSTAMP(t2);
 #ifndef KNN_ABLATE_NO_SLOW
-        if (it > 0) {
-            const float tf = tf_of(tm_prev);
-            if (__ballot(mnY <= tf)) {
-                if constexpr (DEFER) record(Y, it - 1, tf);
-                else { slow(Y, it - 1, tf); dirty = true; }
-            }
+        if (uY) {
+            if constexpr (DEFER) record(Y, it - 1, tf, uY);
+            else { slow(Y, it - 1, tf, uY); dirty = true; }
         }
         if constexpr (DEFER) {
             if ((it & (DEFER_EVERY - 1)) == DEFER_EVERY - 1 && __ballot(qcnt > 0)) {
@@ -494,7 +510,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
             }
         }
 #else
-        asm volatile("" ::"v"(mnY));
+        asm volatile("" ::"s"(uY));
 #endif
         if (LATE_DMA && dma_on) {
 #pragma unroll
@@ -514,15 +530,15 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
         // drain: the last tile's accumulators are in accA (ntiles odd) or accB (even)
         const int last = ntiles - 1;
         auto drain = [&](floatx16 (&Lc)[NACC]) {
-            float m = INF;
+            const float tf = tf_of(tm_prev);
+            uint32_t u = 0u;
 #pragma unroll
             for (int c = 0; c < NACC; c++)
 #pragma unroll
-                for (int r = 0; r < 16; r++) m = fminf(m, Lc[c][r]);
-            const float tf = tf_of(tm_prev);
-            if (__ballot(m <= tf)) {
-                if constexpr (DEFER) record(Lc, last, tf);
-                else slow(Lc, last, tf);
+                for (int r = 0; r < 16; r++) u |= (__ballot(Lc[c][r] <= tf) != 0ull ? 1u : 0u) << (16 * c + r);
+            if (u) {
+                if constexpr (DEFER) record(Lc, last, tf, u);
+                else slow(Lc, last, tf, u);
             }
         };
         if (last & 1) drain(accB);
@@ -568,24 +584,35 @@ bool knn_fused_supported(int d) { return d == 64 || d == 128 || d == 256; }
 FilterPlan knn_fused_plan(int d, int k, const FilterStudy* fs) {
     const int rb = 2 * d + 32;
     const size_t cap = 160 * 1024;
+    // pass-set variant (FilterPlan.qg): in-step for d >= 128; KNN_FILTER_PSTEP overrides (study)
+    const int pstep = fs && fs->pstep >= 0 ? fs->pstep : (d >= 128 ? 1 : 0);
     auto make = [&](int nw, int rg, int minw, int nbuf) {
-        return FilterPlan{nw, 1, rg, minw, nbuf, 32 * nw, fused_lds_of(rb, k, nw, rg, nbuf)};
+        return FilterPlan{nw, pstep, rg, minw, nbuf, 32 * nw, fused_lds_of(rb, k, nw, rg, nbuf)};
     };
     const bool force8 = fs && fs->shape[0] == 'w' && fs->shape[1] == '8';
     const int nb = fs && fs->nbuf == 3 ? 3 : 2;  // kernel study: triple-buffered tiles
-    if (d == 64 && !force8 && fused_lds_of(rb, k, 4, 2, nb) <= cap / 2) return make(4, 2, 2, nb);
+    const bool force4 = fs && fs->shape[0] == 'w' && fs->shape[1] == '4';
+    if ((d == 64 || force4) && !force8 && fused_lds_of(rb, k, 4, 2, nb) <= cap / 2) return make(4, 2, 2, nb);
     if (fused_lds_of(rb, k, 8, 2, nb) <= cap) return make(8, 2, 2, nb);
     if (fused_lds_of(rb, k, 8, 1, 2) <= cap) return make(8, 1, 2, 2);
     return FilterPlan{0, 0, 0, 0, 0, 0, 0};  // k too large for the LDS heaps: not supported
 }
 
+// FilterPlan.qg carries the pass-set variant of the fused kernel: 1 = built in the step
+// (PSTEP: a v_cmp per value between the MFMAs; d >= 128, where the MFMAs hide it), 0 = a
+// v_min3 chain in the step and the set built on passing tiles only (d = 64: 10 MFMAs per
+// tile leave no room).  Measured on one box: A (d = 128) PSTEP faster, B (d = 64) slower.
+template <int RB, bool P>
+static const void* fused_fn_p(const FilterPlan& f) {
+#define KNN_FUSED_FN(NB, NW, RG) reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, NB, NW, RG, P>)
+    if (f.nw == 4) return f.nbuf == 3 ? KNN_FUSED_FN(3, 4, 2) : KNN_FUSED_FN(2, 4, 2);
+    if (f.rg == 2) return f.nbuf == 3 ? KNN_FUSED_FN(3, 8, 2) : KNN_FUSED_FN(2, 8, 2);
+    return KNN_FUSED_FN(2, 8, 1);
+#undef KNN_FUSED_FN
+}
 template <int RB>
 static const void* fused_fn(const FilterPlan& f) {
-    if (f.nw == 4) return f.nbuf == 3 ? reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, 3, 4, 2>)
-                                      : reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, 2, 4, 2>);
-    if (f.rg == 2) return f.nbuf == 3 ? reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, 3, 8, 2>)
-                                      : reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, 2, 8, 2>);
-    return reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, 2, 8, 1>);
+    return f.qg ? fused_fn_p<RB, true>(f) : fused_fn_p<RB, false>(f);
 }
 
 static const void* fused_ptr(int d, const FilterPlan& f) {

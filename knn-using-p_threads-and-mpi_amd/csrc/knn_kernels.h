@@ -122,7 +122,7 @@ bool knn_gemm_filter_supported(int elem, int row_bytes);
 struct FilterPlan { int nw, qg, rg, minw, nbuf, bm; size_t lds; };
 // kernel-study overrides of the plan (KNN_FILTER_NBUF / KNN_FILTER_SHAPE, read once per
 // context by knn_create); NULL = the product plan
-struct FilterStudy { int nbuf; char shape[8]; };
+struct FilterStudy { int nbuf; char shape[8]; int pstep; /* -1 = plan default */ };
 FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k, const FilterStudy* fs = nullptr);
 hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st,
                                   const FilterStudy* fs = nullptr);
