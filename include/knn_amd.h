@@ -22,13 +22,14 @@
 #ifndef KNN_AMD_H
 #define KNN_AMD_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define KNN_AMD_ABI_VERSION 1
+#define KNN_AMD_ABI_VERSION 2
 
 typedef enum {
     KNN_OK = 0,
@@ -61,12 +62,19 @@ typedef enum {
                                 per-query fallback) */
 } knn_algo;
 
-/* Context options.  One context drives one device (one HIP stream). */
+/* knn_opts.flags */
+#define KNN_OPT_CACHE_TRAIN 1  /* knn_predict keeps the device copy of train across calls, keyed
+                                  by (feat, labels, n, d, ld, dtype) and the generation set by
+                                  knn_set_generation: a caller that rewrites a train buffer in
+                                  place bumps the generation */
+
+/* Context options.  One context drives one device (a compute stream and a copy stream). */
 typedef struct {
     int32_t device;        /* HIP device ordinal */
     int32_t algo;          /* knn_algo */
     int32_t train_splits;  /* GEMM path: train segments per query tile (0 = auto) */
     int32_t profile;       /* 1 = record per-stage HIP events (knn_stage_times) */
+    int32_t flags;         /* KNN_OPT_* */
 } knn_opts;
 
 /* A dataset view.  feat: row-major [n][ld] of dtype; labels: int32 [n] (train only). */
@@ -92,6 +100,17 @@ void knn_destroy(knn_ctx* ctx);
 /* Text of the last error on this context ("" if none). */
 const char* knn_last_error(const knn_ctx* ctx);
 
+/* Invalidates cached train uploads (KNN_OPT_CACHE_TRAIN): the cache key includes this
+ * generation.  The reference has no counterpart (every KNN() call re-reads ArffData,
+ * main.cpp:40-43). */
+knn_status knn_set_generation(knn_ctx* ctx, uint64_t generation);
+
+/* Page-locked host memory for datasets and outputs of knn_predict: copies from/to it run
+ * as asynchronous DMA, overlapping the device's compute (pageable buffers work too, at
+ * the runtime's staged rate). */
+knn_status knn_alloc_pinned(size_t bytes, void** out);
+void knn_free_pinned(void* p);
+
 /*
  * Host-buffer entry point.  Replaces `int* KNN(ArffData* train, ArffData* test, int k)`
  * (main.cpp:25) for queries [0, test->n) and the MPI variant
@@ -102,6 +121,11 @@ const char* knn_last_error(const knn_ctx* ctx);
  * k must satisfy 1 <= k <= train->n (the reference crashes for k > n_train and
  * returns all-zero predictions for k <= 0; the C++ KNN() wrapper reproduces the
  * latter, the ABI reports KNN_EINVAL).
+ * Data movement: train is uploaded once per call, or once per context with
+ * KNN_OPT_CACHE_TRAIN; queries stream through two device slots in batches -- batch b+1
+ * uploads on the context's copy stream while batch b computes, and batch b's results
+ * download while b+1 computes.  knn_last_stats()[6] / [7] report the train / query bytes
+ * this call moved host -> device.
  */
 knn_status knn_predict(knn_ctx* ctx, const knn_dataset* train, const knn_dataset* test,
                        int32_t k, int32_t num_classes, int64_t q_begin, int64_t q_end,
@@ -150,8 +174,9 @@ int32_t knn_stage_times(const knn_ctx* ctx, const char** names, float* ms, int32
  * the exact fallback, [2] train segments used, [3] filter operand type (-1 = no GEMM
  * filter ran, 0 = fp32, 1 = bf16, 2 = bf16 hi/lo split of fp32, 3 = bf16 rounding of
  * fp32), [4] 1 when AUTO re-ran the call with the split filter, [5] 1 when the filter
- * ran with the train norm folded into the MFMA (the fused-norm bf16 filter).  Returns the
- * number written. */
+ * ran with the train norm folded into the MFMA (the fused-norm bf16 filter), [6] train
+ * bytes and [7] query bytes a knn_predict call copied host -> device.  Returns the number
+ * written (<= 8). */
 int32_t knn_last_stats(const knn_ctx* ctx, int64_t* out, int32_t n);
 
 /*

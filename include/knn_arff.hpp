@@ -17,12 +17,15 @@
 #ifndef KNN_ARFF_HPP
 #define KNN_ARFF_HPP
 
+#include <cstddef>
 #include <cstdint>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
+
+#include "knn_amd.h"
 
 typedef long int int32;   // libarff/arff_utils.h:16 (8 bytes on LP64, as in the reference)
 typedef long long int64;  // libarff/arff_utils.h:18
@@ -77,10 +80,38 @@ private:
     std::vector<ArffValue*> m_data;
 };
 
+// Page-locked host storage for the flat view (knn_alloc_pinned), so KNN()'s uploads run as
+// asynchronous DMA; plain heap memory when no device can pin it.  A 16-byte header records
+// which allocator owns the block.
+template <typename T>
+struct KnnPinnedAllocator {
+    typedef T value_type;
+    KnnPinnedAllocator() = default;
+    template <typename U>
+    KnnPinnedAllocator(const KnnPinnedAllocator<U>&) {}
+    T* allocate(size_t n) {
+        void* p = nullptr;
+        const size_t bytes = n * sizeof(T) + 16;
+        bool pinned = knn_alloc_pinned(bytes, &p) == KNN_OK && p;
+        if (!pinned) p = ::operator new(bytes);
+        *static_cast<int*>(p) = pinned ? 1 : 0;
+        return reinterpret_cast<T*>(static_cast<char*>(p) + 16);
+    }
+    void deallocate(T* t, size_t) {
+        char* p = reinterpret_cast<char*>(t) - 16;
+        if (*reinterpret_cast<int*>(p)) knn_free_pinned(p);
+        else ::operator delete(p);
+    }
+    template <typename U>
+    bool operator==(const KnnPinnedAllocator<U>&) const { return true; }
+    template <typename U>
+    bool operator!=(const KnnPinnedAllocator<U>&) const { return false; }
+};
+
 // Flat, KNN-ready view of a dataset (features [n][ld] row-major, ld = d rounded up to 4).
 struct KnnFlatView {
-    std::vector<float> feat;
-    std::vector<int32_t> labels;   // (int)(float) of the class attribute (main.cpp:66)
+    std::vector<float, KnnPinnedAllocator<float>> feat;
+    std::vector<int32_t, KnnPinnedAllocator<int32_t>> labels;   // (int)(float) of the class attribute (main.cpp:66)
     int64_t n = 0;
     int d = 0;
     int ld = 0;

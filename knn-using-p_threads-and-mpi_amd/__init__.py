@@ -42,9 +42,12 @@ class KnnError(RuntimeError):
         super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
 
 
+KNN_OPT_CACHE_TRAIN = 1
+
+
 class knn_opts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("algo", ctypes.c_int32),
-                ("train_splits", ctypes.c_int32), ("profile", ctypes.c_int32)]
+                ("train_splits", ctypes.c_int32), ("profile", ctypes.c_int32), ("flags", ctypes.c_int32)]
 
 
 class knn_dataset(ctypes.Structure):
@@ -88,6 +91,9 @@ def load_library(path=LIB_PATH):
         "knn_generate": (I32, [P, P, P, I64, I64, I32, I32, I32, I32, ctypes.c_uint64,
                                ctypes.c_uint32, I32, P]),
         "knn_mfma_probe_bf16": (I32, [P, P, P, I32, P, P]),
+        "knn_set_generation": (I32, [P, ctypes.c_uint64]),
+        "knn_alloc_pinned": (I32, [ctypes.c_size_t, ctypes.POINTER(P)]),
+        "knn_free_pinned": (None, [P]),
         "knn_confusion_matrix": (I32, [P, P, I64, I32, P]),
         "knn_confusion_matrix_device": (I32, [P, P, P, I64, I32, P, P, P]),
         "knn_accuracy": (F, [P, I32, I64]),
@@ -264,10 +270,12 @@ def train_sharded_predict(ctx, train_shard, labels_shard, idx_base, test, k, num
 class Context:
     """One device, one HIP stream (knn_create / knn_destroy)."""
 
-    def __init__(self, device=0, algo="auto", train_splits=0, profile=False):
+    def __init__(self, device=0, algo="auto", train_splits=0, profile=False, cache_train=False):
         self.lib = load_library()
         # profile: False/0 off, True/1 per-stage HIP events, 2 = also count filter candidates
-        opts = knn_opts(device, ALGOS[algo], train_splits, int(profile))
+        # cache_train: predict() keeps the device copy of train across calls (KNN_OPT_CACHE_TRAIN)
+        opts = knn_opts(device, ALGOS[algo], train_splits, int(profile),
+                        KNN_OPT_CACHE_TRAIN if cache_train else 0)
         h = ctypes.c_void_p()
         st = self.lib.knn_create(ctypes.byref(h), ctypes.byref(opts))
         if st != KNN_OK:
@@ -381,10 +389,14 @@ class Context:
                                                  None if stream is None else ctypes.c_void_p(stream)))
         return out
 
+    def set_generation(self, generation):
+        """Invalidate cached train uploads (knn_set_generation)."""
+        self._check(self.lib.knn_set_generation(self.h, generation))
+
     def stage_times(self):
-        names = (ctypes.c_char_p * 16)()
-        ms = (ctypes.c_float * 16)()
-        n = self.lib.knn_stage_times(self.h, names, ms, 16)
+        names = (ctypes.c_char_p * 256)()
+        ms = (ctypes.c_float * 256)()
+        n = self.lib.knn_stage_times(self.h, names, ms, 256)
         out = {}
         for i in range(n):
             key = names[i].decode()
@@ -392,11 +404,39 @@ class Context:
         return out
 
     def stats(self):
-        v = (ctypes.c_int64 * 6)()
-        self.lib.knn_last_stats(self.h, v, 6)
+        v = (ctypes.c_int64 * 8)()
+        self.lib.knn_last_stats(self.h, v, 8)
         return {"candidates": v[0], "fallback_queries": v[1], "train_segments": v[2],
                 "filter_operands": FILTER_OPERANDS.get(v[3], v[3]), "rerun_split": bool(v[4]),
-                "fused_norm": bool(v[5])}
+                "fused_norm": bool(v[5]), "h2d_train_bytes": v[6], "h2d_query_bytes": v[7]}
+
+
+class PinnedArray:
+    """A numpy array over page-locked host memory (knn_alloc_pinned / knn_free_pinned)."""
+
+    def __init__(self, shape, dtype):
+        self.lib = load_library()
+        dtype = np.dtype(dtype)
+        nbytes = int(np.prod(shape)) * dtype.itemsize
+        p = ctypes.c_void_p()
+        st = self.lib.knn_alloc_pinned(max(nbytes, 1), ctypes.byref(p))
+        if st != KNN_OK:
+            raise KnnError(st, f"knn_alloc_pinned({nbytes})")
+        self.ptr = p
+        buf = (ctypes.c_char * max(nbytes, 1)).from_address(p.value)
+        self.array = np.frombuffer(buf, dtype=dtype, count=int(np.prod(shape))).reshape(shape)
+
+    def free(self):
+        if getattr(self, "ptr", None):
+            self.array = None
+            self.lib.knn_free_pinned(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 _default_ctx = None

@@ -376,7 +376,7 @@ std::vector<knn_ctx*>& contexts() {
     if (D.ctx.empty()) {
         int n = knn_amd_num_devices();
         for (int i = 0; i < n; i++) {
-            knn_opts o{i, KNN_ALGO_AUTO, 0, 0};
+            knn_opts o{i, KNN_ALGO_AUTO, 0, 0, KNN_OPT_CACHE_TRAIN};  // ArffData is immutable once parsed
             knn_ctx* c = nullptr;
             knn_status s = knn_create(&c, &o);
             if (s != KNN_OK) {

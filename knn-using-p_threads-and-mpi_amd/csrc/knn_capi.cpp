@@ -68,12 +68,26 @@ struct knn_ctx {
     // host-API staging (device copies of host inputs / outputs)
     DBuf h_train, h_labels, h_test, h_pred, h_dist, h_idx;
     int32_t* ctrl_host = nullptr;  // pinned: [0] status, [1] fallback count
+    // host-buffer calls (knn_predict): cached train upload, two query slots streamed on a copy stream
+    int cache_train = 0;
+    uint64_t generation = 0;
+    struct { const void* feat; const int32_t* labels; int64_t n; int d, ld, dtype, ldd; uint64_t gen; bool valid; }
+        tcache{nullptr, nullptr, 0, 0, 0, 0, 0, 0, false};
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_up[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr}, ev_down[2] = {nullptr, nullptr};
+    DBuf q_slot[2], pred_slot[2], dist_slot[2], idx_slot[2];
+    std::vector<int32_t*> ctrl_slots;  // pinned copies of the status word, one per batch
+    int64_t batch_rows = 131072;       // queries per streamed batch of a host-buffer call
+    int64_t ws_queries = 1 << 22;      // GEMM-path queries per pass (candidate workspace budget)
+    int64_t h2d_train = 0, h2d_query = 0;
     // profiling
     std::vector<hipEvent_t> events;
     std::vector<Stage> stages;
     std::vector<float> stage_ms;
     std::vector<const char*> stage_names;
-    int64_t stats[6] = {0, 0, 0, -1, 0, 0};  // candidates, fallback queries, segments, filter operand type, rerun, fused
+    int64_t stats[8] = {0, 0, 0, -1, 0, 0, 0, 0};  // candidates, fallback queries, segments, filter operand
+                                                   // type, rerun, fused, train / query H2D bytes
+    int64_t rerun_stats[3] = {0, -1, 0};    // segments, operand type, fused of AUTO's gated split re-run
     int num_cus = 256;
 };
 
@@ -166,23 +180,32 @@ int choose_algo(const knn_ctx* c, int64_t nt, int64_t nq, int d, int k, int dtyp
     return KNN_ALGO_DIRECT;
 }
 
-knn_status finish_call(knn_ctx* c, hipStream_t st) {
-    HIP_OR_FAIL(c, hipMemcpyAsync(c->ctrl_host, c->ctrl.p, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    HIP_OR_FAIL(c, hipStreamSynchronize(st));
-    if (c->profile) {
-        c->stage_ms.clear();
-        c->stage_names.clear();
-        for (auto& s : c->stages) {
-            float ms = 0.f;
-            (void)hipEventElapsedTime(&ms, s.a, s.b);
-            c->stage_ms.push_back(ms);
-            c->stage_names.push_back(s.name);
-        }
+// per-stage times of the drained stream (profile mode)
+void collect_stages(knn_ctx* c) {
+    if (!c->profile) return;
+    c->stage_ms.clear();
+    c->stage_names.clear();
+    for (auto& s : c->stages) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, s.a, s.b);
+        c->stage_ms.push_back(ms);
+        c->stage_names.push_back(s.name);
     }
-    int32_t status = c->ctrl_host[0];
+}
+
+knn_status check_status(knn_ctx* c, const int32_t* ctrl) {
+    const int32_t status = ctrl[0];
     if (status & KNN_STATUS_BAD_LABEL) return fail(c, KNN_EINVAL, "a train label is outside [0, num_classes)");
     if (status & KNN_STATUS_TOO_FEW) return fail(c, KNN_ERANGE, "fewer than k train rows have a finite distance (< FLT_MAX)");
     return KNN_OK;
+}
+
+// the one host synchronisation of a call: status word to the host, stream drained
+knn_status finish_call(knn_ctx* c, hipStream_t st) {
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->ctrl_host, c->ctrl.p, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(c, hipStreamSynchronize(st));
+    collect_stages(c);
+    return check_status(c, c->ctrl_host);
 }
 
 // k_direct_tile segments: enough (query block, segment) units to fill whole waves of
@@ -327,9 +350,13 @@ int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int
     return best;
 }
 
+// The GEMM pipeline of one filter operand type, enqueued on st with no host round trip:
+// norms -> operand rows -> filter -> rescore (queries whose candidate list overflowed, or
+// every query when a norm is too large for the certificate, go to the fallback list).
+// gate (optional): every stage runs only when *gate != 0 (AUTO's re-run, decided on the
+// device by k_rerun_decide).  The fallback scan is enqueued by the caller.
 knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int k, int C,
-                    const QueryOut& out, hipStream_t st, int algo, bool* fell_back, int64_t retry_limit = -1) {
-    *fell_back = false;
+                    const QueryOut& out, hipStream_t st, int algo, const int32_t* gate) {
     const int64_t nt = tr->n, nq = te->n;
     const int d = tr->d;
     const int dtype = tr->dtype;
@@ -357,27 +384,18 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     } else {
         certificate(d, felem, &coef, &eta);
     }
-    stage_begin(c, st, "norms");
+    stage_begin(c, st, gate ? "norms_rerun" : "norms");
     HIP_OR_FAIL(c, knn_launch_row_norms(tr->feat, dtype, nt, tr->ld, d, c->tnorm.as<float>(),
                                         c->ctrl.as<int32_t>(), c->ctrl.as<uint32_t>() + 2,
-                                        c->tnp.as<float>(), 1.0f - coef, st, fused ? c->tmax.as<float>() : nullptr));
+                                        c->tnp.as<float>(), 1.0f - coef, st, fused ? c->tmax.as<float>() : nullptr,
+                                        gate));
     HIP_OR_FAIL(c, knn_launch_row_norms(te->feat, dtype, nq, te->ld, d, c->qnorm.as<float>(),
-                                        c->ctrl.as<int32_t>(), nullptr, nullptr, 0.0f, st));
+                                        c->ctrl.as<int32_t>(), nullptr, nullptr, 0.0f, st, nullptr, gate));
     stage_end(c, st);
-    // the certificate needs every norm < 2^125; otherwise take the exact path
-    HIP_OR_FAIL(c, hipMemcpyAsync(c->ctrl_host, c->ctrl.p, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    HIP_OR_FAIL(c, hipStreamSynchronize(st));
-    if (c->ctrl_host[0] & KNN_STATUS_GEMM_UNSAFE) {
-        HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st));
-        *fell_back = true;
-        stage_begin(c, st, "direct_tile");
-        knn_status s = run_direct_tile(c, tr, te, k, C, out, st);
-        stage_end(c, st);
-        return s;
-    }
-
-    stage_begin(c, st, "filter_init");
-    HIP_OR_FAIL(c, hipMemsetD32Async((hipDeviceptr_t)c->gthr.p, 0xFF800000u, nq, st));  // ordered(+inf)
+    // (a norm >= 2^125 sets GEMM_UNSAFE in the status word: the filter then skips and the
+    // rescore sends every query to the exact fallback scan -- decided on the device)
+    stage_begin(c, st, gate ? "filter_init_rerun" : "filter_init");
+    HIP_OR_FAIL(c, knn_launch_fill_u32(c->gthr.as<uint32_t>(), nq, 0xFF800000u, gate, st));  // ordered(+inf)
     stage_end(c, st);
     // study option KNN_FILTER_SEED=1: starting thresholds from the exact k-th distance to a
     // spread sample of train rows (k_seed_threshold), so the first segment does not begin
@@ -392,7 +410,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         sa.test = te->feat; sa.nq = nq; sa.ld_q = te->ld; sa.d = d; sa.k = k;
         sa.ns = (int)ns; sa.ld_lds = (d + 3) & ~3;
         sa.gthr = c->gthr.as<uint32_t>();
-        stage_begin(c, st, "seed");
+        stage_begin(c, st, gate ? "seed_rerun" : "seed");
         HIP_OR_FAIL(c, knn_launch_seed_threshold(sa, dtype, st));
         stage_end(c, st);
     }
@@ -405,29 +423,29 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         // augmented bf16 rows: train [rn(t) | tn split], queries [-2 rn(q) | 1 1 1]
         HIP_OR_FAIL(c, c->split_t.ensure(sizeof(uint16_t) * (size_t)(d + 16) * nt));
         HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * (size_t)(d + 16) * nq));
-        stage_begin(c, st, "aug");
+        stage_begin(c, st, gate ? "aug_rerun" : "aug");
         HIP_OR_FAIL(c, knn_launch_aug_rows(tr->feat, dtype, nt, tr->ld, d, c->tnorm.as<float>(), 1.0f,
-                                           c->split_t.as<uint16_t>(), st));
+                                           c->split_t.as<uint16_t>(), st, gate));
         HIP_OR_FAIL(c, knn_launch_aug_rows(te->feat, dtype, nq, te->ld, d, nullptr, -2.0f,
-                                           c->split_q.as<uint16_t>(), st));
+                                           c->split_q.as<uint16_t>(), st, gate));
         stage_end(c, st);
         ftrain = c->split_t.p; ftest = c->split_q.p;
         fld_t = fld_q = d + 16;
     } else if (felem == ELEM_SPLIT) {
         HIP_OR_FAIL(c, c->split_t.ensure(sizeof(uint16_t) * 2 * d * nt));
         HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * 2 * d * nq));
-        stage_begin(c, st, "split");
-        HIP_OR_FAIL(c, knn_launch_split_rows((const float*)tr->feat, nt, tr->ld, d, c->split_t.as<uint16_t>(), st));
-        HIP_OR_FAIL(c, knn_launch_split_rows((const float*)te->feat, nq, te->ld, d, c->split_q.as<uint16_t>(), st));
+        stage_begin(c, st, gate ? "split_rerun" : "split");
+        HIP_OR_FAIL(c, knn_launch_split_rows((const float*)tr->feat, nt, tr->ld, d, c->split_t.as<uint16_t>(), st, gate));
+        HIP_OR_FAIL(c, knn_launch_split_rows((const float*)te->feat, nq, te->ld, d, c->split_q.as<uint16_t>(), st, gate));
         stage_end(c, st);
         ftrain = c->split_t.p; ftest = c->split_q.p;
         fld_t = fld_q = 2 * d;
     } else if (felem == ELEM_ROUND) {
         HIP_OR_FAIL(c, c->split_t.ensure(sizeof(uint16_t) * d * nt));
         HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * d * nq));
-        stage_begin(c, st, "round");
-        HIP_OR_FAIL(c, knn_launch_round_rows((const float*)tr->feat, nt, tr->ld, d, c->split_t.as<uint16_t>(), st));
-        HIP_OR_FAIL(c, knn_launch_round_rows((const float*)te->feat, nq, te->ld, d, c->split_q.as<uint16_t>(), st));
+        stage_begin(c, st, gate ? "round_rerun" : "round");
+        HIP_OR_FAIL(c, knn_launch_round_rows((const float*)tr->feat, nt, tr->ld, d, c->split_t.as<uint16_t>(), st, gate));
+        HIP_OR_FAIL(c, knn_launch_round_rows((const float*)te->feat, nq, te->ld, d, c->split_q.as<uint16_t>(), st, gate));
         stage_end(c, st);
         ftrain = c->split_t.p; ftest = c->split_q.p;
         fld_t = fld_q = d;
@@ -449,6 +467,8 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     g.cnt = c->cnt.as<int32_t>(); g.cand_idx = c->cand_idx.as<int32_t>();
     g.cand_L = c->cand_L.as<float>(); g.cand_U = c->cand_U.as<float>(); g.cap = cap; g.cap_seg = cap / nseg;
     g.tmax = fused ? c->tmax.as<float>() : nullptr;
+    g.status = c->ctrl.as<int32_t>();
+    g.gate = gate;
     // kernel studies: KNN_FILTER_TIMING=1 with a -DKNN_FILTER_TIMING build prints the
     // filter's per-phase shader clocks per wave (wait+barrier, DMA issue, step, slow path)
     const bool timing = c->study_timing != 0;
@@ -457,7 +477,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         HIP_OR_FAIL(c, hipMemsetAsync(c->timing.p, 0, 16 * sizeof(unsigned long long), st));
         g.timing = c->timing.as<unsigned long long>();
     }
-    stage_begin(c, st, "gemm_filter");
+    stage_begin(c, st, gate ? "gemm_filter_rerun" : "gemm_filter");
     if (fused) HIP_OR_FAIL(c, knn_launch_fused(g, st, &c->fstudy));
     else HIP_OR_FAIL(c, knn_launch_gemm_filter(g, kelem, rb, st, &c->fstudy));
     stage_end(c, st);
@@ -478,26 +498,21 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     r.nseg = 2 * nseg; r.cap_seg = g.cap_seg / 2;  // sub-slices: (segment, lane half)
     r.out = out; r.status = c->ctrl.as<int32_t>();
     r.fb_list = c->fb_list.as<int32_t>(); r.fb_count = c->ctrl.as<int32_t>() + 1;
-    stage_begin(c, st, "rescore");
+    r.gate = gate;
+    stage_begin(c, st, gate ? "rescore_rerun" : "rescore");
     HIP_OR_FAIL(c, knn_launch_rescore(r, st));
     stage_end(c, st);
 
-    c->stats[2] = nseg;
-    c->stats[3] = felem;
-    c->stats[5] = fused;
-    if (retry_limit >= 0) {
-        // AUTO's rounded filter: too many overflowing queries -> the caller re-runs as split
-        HIP_OR_FAIL(c, hipMemcpyAsync(c->ctrl_host, c->ctrl.p, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-        HIP_OR_FAIL(c, hipStreamSynchronize(st));
-        if (c->ctrl_host[1] > retry_limit) {
-            *fell_back = true;
-            return KNN_OK;
-        }
+    if (!gate) {
+        c->stats[2] = nseg;
+        c->stats[3] = felem;
+        c->stats[5] = fused;
+    } else {
+        c->rerun_stats[0] = nseg;
+        c->rerun_stats[1] = felem;
+        c->rerun_stats[2] = fused;
     }
-    stage_begin(c, st, "fallback_scan");
-    knn_status s = run_exact_scan(c, tr, te, k, C, out, st, r.fb_list, r.fb_count);
-    stage_end(c, st);
-    return s;
+    return KNN_OK;
 }
 
 }  // namespace
@@ -518,6 +533,7 @@ knn_status knn_create(knn_ctx** out, const knn_opts* opts) {
         c->algo = opts->algo;
         c->train_splits = opts->train_splits;
         c->profile = opts->profile;
+        c->cache_train = (opts->flags & KNN_OPT_CACHE_TRAIN) != 0;
     }
     // kernel-study switches (DESIGN.md "Ablation builds"): read here once, never per call
     if (const char* e = getenv("KNN_FILTER_SEED")) c->study_seed = atoi(e);
@@ -539,11 +555,26 @@ knn_status knn_create(knn_ctx** out, const knn_opts* opts) {
     }
     c->num_cus = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&c->ctrl_host, 4 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess ||
         c->ctrl.ensure(4 * sizeof(int32_t)) != hipSuccess) {
         knn_destroy(c);
         return KNN_EHIP;
     }
+    for (int i = 0; i < 2; i++)
+        if (hipEventCreateWithFlags(&c->ev_up[i], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_done[i], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_down[i], hipEventDisableTiming) != hipSuccess) {
+            knn_destroy(c);
+            return KNN_EHIP;
+        }
+    // GEMM-path candidate workspace: 12 B x 64 CAPW per query; passes of at most a quarter of
+    // the free HBM (KNN_WS_QUERIES / KNN_BATCH_ROWS override, for tests)
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
+        c->ws_queries = std::max<int64_t>(4096, (int64_t)(free_b / 4) / (12 * 64 * KNN_RESCORE_CAPW + 64));
+    if (const char* e = getenv("KNN_WS_QUERIES")) c->ws_queries = std::max<int64_t>(1, atoll(e));
+    if (const char* e = getenv("KNN_BATCH_ROWS")) c->batch_rows = std::max<int64_t>(1, atoll(e));
     *out = c;
     return KNN_OK;
 }
@@ -556,8 +587,15 @@ void knn_destroy(knn_ctx* c) {
                     &c->h_dist, &c->h_idx})
         b->release();
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
+    for (int i = 0; i < 2; i++) {
+        for (hipEvent_t e : {c->ev_up[i], c->ev_done[i], c->ev_down[i]})
+            if (e) (void)hipEventDestroy(e);
+        for (DBuf* b : {&c->q_slot[i], &c->pred_slot[i], &c->dist_slot[i], &c->idx_slot[i]}) b->release();
+    }
+    for (int32_t* p : c->ctrl_slots) (void)hipHostFree(p);
     if (c->ctrl_host) (void)hipHostFree(c->ctrl_host);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->cstream) (void)hipStreamDestroy(c->cstream);
     delete c;
 }
 
@@ -567,11 +605,9 @@ const char* knn_last_error(const knn_ctx* c) { return c ? c->err.c_str() : "null
 
 namespace {
 
-// Shared validation + pipeline of knn_predict_device / knn_shard_topk_device.
-// shard = true: the train set is one shard of a larger one; k may exceed its rows and
-// queries with fewer than k neighbours are not an error (the merge decides).
-knn_status predict_core(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int32_t k, int32_t C,
-                        const QueryOut& out, void* hip_stream, bool shard) {
+// Validation shared by the device entry points.
+knn_status validate_call(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int32_t k, int32_t C,
+                         const QueryOut& out, bool shard) {
     knn_status s;
     if ((s = check_dataset(c, tr, "train", true)) != KNN_OK) return s;
     if ((s = check_dataset(c, te, "test", false)) != KNN_OK) return s;
@@ -588,28 +624,33 @@ knn_status predict_core(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te
         (((uintptr_t)te->feat) & 15))
         return fail(c, KNN_EINVAL, "device rows must be 16-byte aligned (ld * element size %% 16 == 0)");
     if (te->n > 0 && !shard && !out.pred) return fail(c, KNN_EINVAL, "pred is NULL");
-    HIP_OR_FAIL(c, hipSetDevice(c->device));
-    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
-    c->stages.clear();
-    c->stats[0] = c->stats[1] = c->stats[2] = c->stats[4] = c->stats[5] = 0;
-    c->stats[3] = -1;
-    if (te->n == 0) return KNN_OK;
+    return KNN_OK;
+}
+
+// One pass of the pipeline over a query set, enqueued on st with no host synchronisation;
+// the status word is copied to ctrl_copy (pinned host, optional) at the end.
+knn_status predict_enqueue(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int32_t k, int32_t C,
+                           const QueryOut& out, hipStream_t st, int algo, int32_t* ctrl_copy) {
+    knn_status s;
     HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st));
-    int algo = choose_algo(c, tr->n, te->n, tr->d, k, tr->dtype);
-    const bool gemm = is_gemm(algo);
-    if (gemm) {
-        bool fb = false;
+    if (is_gemm(algo)) {
         // AUTO on fp32 data runs the rounded filter first; when more than 1/16 of the queries
         // (at least 256) overflow its candidate lists, the call is re-run with the split
-        // filter (every output is rewritten; the fallback scan of the first run is skipped)
+        // filter (every output is rewritten).  The decision is made on the device
+        // (k_rerun_decide): the split stages are enqueued behind a gate, so a call ends in a
+        // single stream synchronisation either way.
         const bool adaptive = c->algo == KNN_ALGO_AUTO && filter_elem(algo, tr->dtype) == ELEM_ROUND;
-        const int64_t limit = adaptive ? std::max<int64_t>(256, te->n / 16) : -1;
-        if ((s = run_gemm(c, tr, te, k, C, out, st, algo, &fb, limit)) != KNN_OK) return s;
-        if (adaptive && fb && !(c->ctrl_host[0] & KNN_STATUS_GEMM_UNSAFE)) {
-            HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.as<int32_t>() + 1, 0, sizeof(int32_t), st));
-            c->stats[4] = 1;
-            if ((s = run_gemm(c, tr, te, k, C, out, st, KNN_ALGO_GEMM_SPLIT, &fb)) != KNN_OK) return s;
+        if ((s = run_gemm(c, tr, te, k, C, out, st, algo, nullptr)) != KNN_OK) return s;
+        if (adaptive) {
+            const int64_t limit = std::max<int64_t>(256, te->n / 16);
+            HIP_OR_FAIL(c, knn_launch_rerun_decide(c->ctrl.as<int32_t>(), limit, st));
+            if ((s = run_gemm(c, tr, te, k, C, out, st, KNN_ALGO_GEMM_SPLIT, c->ctrl.as<int32_t>() + 3)) != KNN_OK)
+                return s;
         }
+        stage_begin(c, st, "fallback_scan");
+        if ((s = run_exact_scan(c, tr, te, k, C, out, st, c->fb_list.as<int32_t>(), c->ctrl.as<int32_t>() + 1)) != KNN_OK)
+            return s;
+        stage_end(c, st);
     } else if (algo == KNN_ALGO_DIRECT_SCAN) {
         stage_begin(c, st, "exact_scan");
         if ((s = run_exact_scan(c, tr, te, k, C, out, st, nullptr, nullptr)) != KNN_OK) return s;
@@ -619,18 +660,101 @@ knn_status predict_core(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te
         if ((s = run_direct_tile(c, tr, te, k, C, out, st)) != KNN_OK) return s;
         stage_end(c, st);
     }
-    s = finish_call(c, st);
-    c->stats[1] = c->ctrl_host[1];
+    if (ctrl_copy) HIP_OR_FAIL(c, hipMemcpyAsync(ctrl_copy, c->ctrl.p, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    return KNN_OK;
+}
+
+// stats of a finished pass (status word in ctrl)
+void pass_stats(knn_ctx* c, const int32_t* ctrl, bool gemm) {
+    c->stats[1] += ctrl[1];
+    if (gemm && ctrl[3]) {
+        // the split re-run ran: its segments / operand type describe the results
+        c->stats[4] = 1;
+        c->stats[2] = c->rerun_stats[0];
+        c->stats[3] = c->rerun_stats[1];
+        c->stats[5] = c->rerun_stats[2];
+    }
+}
+
+QueryOut offset_out(const QueryOut& o, int64_t q0) {
+    QueryOut r = o;
+    if (r.pred) r.pred += q0;
+    if (r.dist) r.dist += q0 * r.stride;
+    if (r.idx) r.idx += q0 * r.stride;
+    if (r.label) r.label += q0 * r.stride;
+    return r;
+}
+
+knn_dataset offset_rows(const knn_dataset& x, int64_t r0, int64_t n) {
+    knn_dataset r = x;
+    r.feat = (const unsigned char*)x.feat + (size_t)r0 * (size_t)x.ld * (size_t)elem_size(x.dtype);
+    r.n = n;
+    return r;
+}
+
+void reset_stats(knn_ctx* c) {
+    c->stages.clear();
+    for (int i = 0; i < 8; i++) c->stats[i] = 0;
+    c->stats[3] = -1;
+}
+
+// Shared pipeline of knn_predict_device / knn_shard_topk_device: the GEMM path runs the
+// queries in passes of at most c->ws_queries (the candidate workspace, 24 KB per query, is
+// bounded by a quarter of the free HBM), each ending in one synchronisation.
+// shard = true: the train set is one shard of a larger one; k may exceed its rows and
+// queries with fewer than k neighbours are not an error (the merge decides).
+knn_status predict_core(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int32_t k, int32_t C,
+                        const QueryOut& out, void* hip_stream, bool shard) {
+    knn_status s;
+    if ((s = validate_call(c, tr, te, k, C, out, shard)) != KNN_OK) return s;
+    HIP_OR_FAIL(c, hipSetDevice(c->device));
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    reset_stats(c);
+    if (te->n == 0) return KNN_OK;
+    const int algo = choose_algo(c, tr->n, te->n, tr->d, k, tr->dtype);
+    const bool gemm = is_gemm(algo);
+    const int64_t pass = gemm ? std::max<int64_t>(1, c->ws_queries) : te->n;
+    for (int64_t q0 = 0; q0 < te->n; q0 += pass) {
+        const knn_dataset tq = offset_rows(*te, q0, std::min(pass, te->n - q0));
+        if ((s = predict_enqueue(c, tr, &tq, k, C, offset_out(out, q0), st, algo, nullptr)) != KNN_OK) return s;
+        if ((s = finish_call(c, st)) != KNN_OK) return s;
+        pass_stats(c, c->ctrl_host, gemm);
+    }
     if (c->profile >= 2 && gemm) {
-        // diagnostic only: total candidates kept by the filter
-        std::vector<int32_t> h(te->n * 2 * c->stats[2]);
+        // diagnostic only: total candidates kept by the filter (last pass)
+        std::vector<int32_t> h(std::min(pass, te->n) * 2 * c->stats[2]);
         if (hipMemcpy(h.data(), c->cnt.p, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost) == hipSuccess) {
             int64_t tot = 0;
             for (int32_t v : h) tot += v;
             c->stats[0] = tot;
         }
     }
-    return s;
+    return KNN_OK;
+}
+
+// The train set of a host-buffer call on the device: reused across calls when the context
+// caches train uploads (KNN_OPT_CACHE_TRAIN) and the buffer, shape and generation match.
+knn_status train_device(knn_ctx* c, const knn_dataset* tr, hipStream_t st, knn_dataset* dtr) {
+    const size_t es = (size_t)elem_size(tr->dtype);
+    const int per16 = (int)(16 / es);
+    const int ldd = (tr->d + per16 - 1) / per16 * per16;  // device rows padded to 16 B
+    auto& tc = c->tcache;
+    const bool hit = c->cache_train && tc.valid && tc.feat == tr->feat && tc.labels == tr->labels && tc.n == tr->n &&
+                     tc.d == tr->d && tc.ld == tr->ld && tc.dtype == tr->dtype && tc.gen == c->generation;
+    if (!hit) {
+        tc.valid = false;
+        HIP_OR_FAIL(c, c->h_train.ensure(es * (size_t)ldd * tr->n));
+        HIP_OR_FAIL(c, c->h_labels.ensure(sizeof(int32_t) * tr->n));
+        HIP_OR_FAIL(c, hipMemcpy2DAsync(c->h_train.p, es * ldd, tr->feat, es * tr->ld, es * tr->d, tr->n,
+                                        hipMemcpyHostToDevice, st));
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->h_labels.p, tr->labels, sizeof(int32_t) * tr->n, hipMemcpyHostToDevice, st));
+        c->stats[6] += (int64_t)(es * tr->d * tr->n + sizeof(int32_t) * tr->n);
+        if (c->cache_train) {
+            tc = {tr->feat, tr->labels, tr->n, tr->d, tr->ld, tr->dtype, ldd, c->generation, true};
+        }
+    }
+    *dtr = knn_dataset{c->h_train.p, c->h_labels.as<int32_t>(), tr->n, tr->d, ldd, tr->dtype};
+    return KNN_OK;
 }
 
 }  // namespace
@@ -693,37 +817,99 @@ knn_status knn_predict(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te,
     if (tr->dtype != te->dtype) return fail(c, KNN_EINVAL, "train and test dtypes differ");
     if (k < 1 || k > tr->n) return fail(c, KNN_EINVAL, "k=%d outside [1, n_train=%lld]", k, (long long)tr->n);
     const int64_t nq = q_end - q_begin;
+    reset_stats(c);
     if (nq == 0) return KNN_OK;
     if (!out_pred) return fail(c, KNN_EINVAL, "out_pred is NULL");
     HIP_OR_FAIL(c, hipSetDevice(c->device));
-    const int d = tr->d;
+    hipStream_t st = c->stream, cs = c->cstream;
+    knn_dataset dtr;
+    if ((s = train_device(c, tr, st, &dtr)) != KNN_OK) return s;
+    const int d = tr->d, ldd = dtr.ld;
     const size_t es = (size_t)elem_size(tr->dtype);
-    const int per16 = (int)(16 / es);
-    const int ldd = (d + per16 - 1) / per16 * per16;  // device rows padded to 16 B
-    hipStream_t st = c->stream;
-    HIP_OR_FAIL(c, c->h_train.ensure(es * (size_t)ldd * tr->n));
-    HIP_OR_FAIL(c, c->h_labels.ensure(sizeof(int32_t) * tr->n));
-    HIP_OR_FAIL(c, c->h_test.ensure(es * (size_t)ldd * nq));
-    HIP_OR_FAIL(c, c->h_pred.ensure(sizeof(int32_t) * nq));
-    if (out_dist) HIP_OR_FAIL(c, c->h_dist.ensure(sizeof(float) * nq * k));
-    if (out_idx) HIP_OR_FAIL(c, c->h_idx.ensure(sizeof(int32_t) * nq * k));
-    HIP_OR_FAIL(c, hipMemcpy2DAsync(c->h_train.p, es * ldd, tr->feat, es * tr->ld, es * d, tr->n,
-                                    hipMemcpyHostToDevice, st));
-    HIP_OR_FAIL(c, hipMemcpyAsync(c->h_labels.p, tr->labels, sizeof(int32_t) * tr->n, hipMemcpyHostToDevice, st));
-    HIP_OR_FAIL(c, hipMemcpy2DAsync(c->h_test.p, es * ldd,
-                                    (const unsigned char*)te->feat + es * (size_t)q_begin * te->ld, es * te->ld,
-                                    es * d, nq, hipMemcpyHostToDevice, st));
-    knn_dataset dtr{c->h_train.p, c->h_labels.as<int32_t>(), tr->n, d, ldd, tr->dtype};
-    knn_dataset dte{c->h_test.p, nullptr, nq, d, ldd, te->dtype};
-    s = knn_predict_device(c, &dtr, &dte, k, C, c->h_pred.as<int32_t>(),
-                           out_dist ? c->h_dist.as<float>() : nullptr,
-                           out_idx ? c->h_idx.as<int32_t>() : nullptr, st);
-    if (s != KNN_OK) return s;
-    HIP_OR_FAIL(c, hipMemcpyAsync(out_pred, c->h_pred.p, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, st));
-    if (out_dist) HIP_OR_FAIL(c, hipMemcpyAsync(out_dist, c->h_dist.p, sizeof(float) * nq * k, hipMemcpyDeviceToHost, st));
-    if (out_idx) HIP_OR_FAIL(c, hipMemcpyAsync(out_idx, c->h_idx.p, sizeof(int32_t) * nq * k, hipMemcpyDeviceToHost, st));
+    const int algo = choose_algo(c, tr->n, nq, d, k, tr->dtype);
+    const bool gemm = is_gemm(algo);
+    // queries stream through two device slots: batch b+1 uploads (copy stream) while batch b
+    // computes, and batch b's outputs download while b+1 computes
+    int64_t B = std::min<int64_t>(nq, c->batch_rows);
+    if (gemm) B = std::min<int64_t>(B, c->ws_queries);
+    const int64_t nb = (nq + B - 1) / B;
+    for (int i = 0; i < 2 && i < nb; i++) {
+        HIP_OR_FAIL(c, c->q_slot[i].ensure(es * (size_t)ldd * B));
+        HIP_OR_FAIL(c, c->pred_slot[i].ensure(sizeof(int32_t) * B));
+        if (out_dist) HIP_OR_FAIL(c, c->dist_slot[i].ensure(sizeof(float) * B * k));
+        if (out_idx) HIP_OR_FAIL(c, c->idx_slot[i].ensure(sizeof(int32_t) * B * k));
+    }
+    while ((int64_t)c->ctrl_slots.size() < nb) {
+        int32_t* p = nullptr;
+        HIP_OR_FAIL(c, hipHostMalloc((void**)&p, 4 * sizeof(int32_t), hipHostMallocDefault));
+        c->ctrl_slots.push_back(p);
+    }
+    auto rows = [&](int64_t b) { return std::min(B, nq - b * B); };
+    auto upload = [&](int64_t b) -> knn_status {
+        const int sl = (int)(b & 1);
+        const unsigned char* src = (const unsigned char*)te->feat + es * (size_t)(q_begin + b * B) * (size_t)te->ld;
+        HIP_OR_FAIL(c, hipMemcpy2DAsync(c->q_slot[sl].p, es * ldd, src, es * te->ld, es * d, rows(b),
+                                        hipMemcpyHostToDevice, cs));
+        HIP_OR_FAIL(c, hipEventRecord(c->ev_up[sl], cs));
+        c->stats[7] += (int64_t)(es * d * rows(b));
+        return KNN_OK;
+    };
+    if ((s = upload(0)) != KNN_OK) return s;
+    for (int64_t b = 0; b < nb; b++) {
+        const int sl = (int)(b & 1);
+        HIP_OR_FAIL(c, hipStreamWaitEvent(st, c->ev_up[sl], 0));
+        if (b >= 2) HIP_OR_FAIL(c, hipStreamWaitEvent(st, c->ev_down[sl], 0));  // output slot downloaded
+        const knn_dataset dq{c->q_slot[sl].p, nullptr, rows(b), d, ldd, te->dtype};
+        const QueryOut o{c->pred_slot[sl].as<int32_t>(), out_dist ? c->dist_slot[sl].as<float>() : nullptr,
+                         out_idx ? c->idx_slot[sl].as<int32_t>() : nullptr, nullptr, k, 0};
+        if (b == 0 && (s = validate_call(c, &dtr, &dq, k, C, o, false)) != KNN_OK) return s;
+        if ((s = predict_enqueue(c, &dtr, &dq, k, C, o, st, algo, c->ctrl_slots[b])) != KNN_OK) return s;
+        HIP_OR_FAIL(c, hipEventRecord(c->ev_done[sl], st));
+        if (b + 1 < nb) {
+            if (b + 1 >= 2) HIP_OR_FAIL(c, hipStreamWaitEvent(cs, c->ev_done[(b + 1) & 1], 0));  // slot free
+            if ((s = upload(b + 1)) != KNN_OK) return s;
+        }
+        HIP_OR_FAIL(c, hipStreamWaitEvent(cs, c->ev_done[sl], 0));
+        const int64_t q0 = b * B;
+        HIP_OR_FAIL(c, hipMemcpyAsync(out_pred + q0, c->pred_slot[sl].p, sizeof(int32_t) * rows(b),
+                                      hipMemcpyDeviceToHost, cs));
+        if (out_dist)
+            HIP_OR_FAIL(c, hipMemcpyAsync(out_dist + q0 * k, c->dist_slot[sl].p, sizeof(float) * rows(b) * k,
+                                          hipMemcpyDeviceToHost, cs));
+        if (out_idx)
+            HIP_OR_FAIL(c, hipMemcpyAsync(out_idx + q0 * k, c->idx_slot[sl].p, sizeof(int32_t) * rows(b) * k,
+                                          hipMemcpyDeviceToHost, cs));
+        HIP_OR_FAIL(c, hipEventRecord(c->ev_down[sl], cs));
+    }
+    HIP_OR_FAIL(c, hipStreamSynchronize(cs));
     HIP_OR_FAIL(c, hipStreamSynchronize(st));
+    collect_stages(c);
+    for (int64_t b = 0; b < nb; b++) {
+        if ((s = check_status(c, c->ctrl_slots[b])) != KNN_OK) return s;
+        pass_stats(c, c->ctrl_slots[b], gemm);
+    }
     return KNN_OK;
+}
+
+knn_status knn_set_generation(knn_ctx* c, uint64_t generation) {
+    if (!c) return KNN_EINVAL;
+    c->generation = generation;
+    return KNN_OK;
+}
+
+knn_status knn_alloc_pinned(size_t bytes, void** out) {
+    if (!out) return KNN_EINVAL;
+    *out = nullptr;
+    if (bytes == 0) return KNN_OK;
+    if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+        *out = nullptr;
+        return KNN_ENOMEM;
+    }
+    return KNN_OK;
+}
+
+void knn_free_pinned(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 int32_t knn_stage_times(const knn_ctx* c, const char** names, float* ms, int32_t n) {
@@ -738,7 +924,7 @@ int32_t knn_stage_times(const knn_ctx* c, const char** names, float* ms, int32_t
 
 int32_t knn_last_stats(const knn_ctx* c, int64_t* out, int32_t n) {
     if (!c || !out) return 0;
-    int32_t m = std::min(n, 6);
+    int32_t m = std::min(n, 8);
     for (int32_t i = 0; i < m; i++) out[i] = c->stats[i];
     return m;
 }

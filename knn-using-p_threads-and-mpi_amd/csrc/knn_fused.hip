@@ -45,7 +45,8 @@
 template <typename E>
 __global__ __launch_bounds__(256) void k_aug_rows(const E* __restrict__ x, int64_t n, int ld, int d,
                                                   const float* __restrict__ norms, float scale,
-                                                  bf16_t* __restrict__ out) {
+                                                  bf16_t* __restrict__ out, const int32_t* __restrict__ gate) {
+    if (gate && *gate == 0) return;
     const int per_row = (d + 16) >> 2;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n * per_row) return;
@@ -74,17 +75,17 @@ __global__ __launch_bounds__(256) void k_aug_rows(const E* __restrict__ x, int64
 }
 
 hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int ld, int d, const float* norms, float scale,
-                               uint16_t* out, hipStream_t st) {
+                               uint16_t* out, hipStream_t st, const int32_t* gate) {
     const int64_t total = n * ((d + 16) / 4);
     if (total <= 0) return hipSuccess;
     if (d % 4 || ld % 4) return hipErrorInvalidValue;
     const dim3 grid((unsigned)((total + 255) / 256));
     if (elem == ELEM_BF16)
         hipLaunchKernelGGL(k_aug_rows<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, n, ld, d, norms, scale,
-                           (bf16_t*)out);
+                           (bf16_t*)out, gate);
     else
         hipLaunchKernelGGL(k_aug_rows<float>, grid, dim3(256), 0, st, (const float*)x, n, ld, d, norms, scale,
-                           (bf16_t*)out);
+                           (bf16_t*)out, gate);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -111,6 +112,7 @@ hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int ld, int d
 // ---------------------------------------------------------------------------------
 template <int RB, int MINW, int NBUF, int NW, int RG, bool PSTEP>
 __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) {
+    if ((a.gate && *a.gate == 0) || (*a.status & KNN_STATUS_GEMM_UNSAFE)) return;  // not taken / exact path
     typedef FilterTile<RB, NW, 1, RG> FT;
     constexpr int NACC = RG, BN = FT::BN, BM = FT::BM, STRIDE = FT::STRIDE, SLOTS = FT::SLOTS;
     constexpr int DMA_INS = FT::DMA_INS, TILE = FT::TILE;

@@ -50,6 +50,8 @@ struct GemmFilterArgs {
     int32_t* cnt;  // [nseg][nq] kept rows per (segment, query)
     int32_t* cand_idx; float* cand_L; float* cand_U; int cap; int cap_seg;
     const float* tmax;  // fused filter: per-64-row maximum train norm
+    const int32_t* status;  // the call's status word: a set GEMM_UNSAFE bit skips the filter
+    const int32_t* gate;    // optional: the filter runs only when *gate != 0 (AUTO's re-run)
 };
 
 struct RescoreArgs {
@@ -59,6 +61,7 @@ struct RescoreArgs {
     int nseg; int cap_seg;
     QueryOut out; int32_t* status;
     int32_t* fb_list; int32_t* fb_count;
+    const int32_t* gate;  // optional: runs only when *gate != 0 (AUTO's re-run)
     int q_lds_bytes; int c_lds_bytes; int wave_lds_bytes;  // set by the launcher
 };
 
@@ -111,9 +114,10 @@ struct GenerateArgs {
 hipError_t knn_launch_exact_scan(const ExactScanArgs& a, int grid, hipStream_t st);
 size_t knn_exact_scan_lds(int d, int k, int C);
 // tmax (optional): the maximum norm of every 64-row tile, [ceil(n / 64)] (the fused filter)
+// gate (optional): the stage runs only when *gate != 0 (device-side control of AUTO's re-run)
 hipError_t knn_launch_row_norms(const void* x, int elem, int64_t n, int ld, int d, float* out,
                                 int32_t* status, uint32_t* maxo, float* outp, float c1, hipStream_t st,
-                                float* tmax = nullptr);
+                                float* tmax = nullptr, const int32_t* gate = nullptr);
 // row_bytes = d * element size: 128, 256 or 512
 bool knn_gemm_filter_supported(int elem, int row_bytes);
 // block shape of the filter for (element type, row bytes, k): waves per block, query
@@ -130,8 +134,13 @@ size_t knn_gemm_filter_lds(int elem, int row_bytes, int k, const FilterStudy* fs
 hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks_per_cu,
                                      const FilterStudy* fs = nullptr);
 // fp32 rows [n][ld] (d % 4 == 0) -> bf16 rows [n][2d]: hi = rn(x), lo = rn(x - hi)
-hipError_t knn_launch_split_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st);
-hipError_t knn_launch_round_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st);
+hipError_t knn_launch_split_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st,
+                                 const int32_t* gate = nullptr);
+hipError_t knn_launch_round_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st,
+                                 const int32_t* gate = nullptr);
+hipError_t knn_launch_fill_u32(uint32_t* p, int64_t n, uint32_t v, const int32_t* gate, hipStream_t st);
+// AUTO's re-run decision on the device: ctrl[3] = !unsafe && ctrl[1] > limit (and ctrl[1] = 0 then)
+hipError_t knn_launch_rerun_decide(int32_t* ctrl, int64_t limit, hipStream_t st);
 hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st);
 // fused-norm filter (knn_fused.hip): rows augmented to d + 16 bf16 (k_aug_rows), d in {64, 128, 256}
 bool knn_fused_supported(int d);
@@ -140,7 +149,7 @@ hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu, const FilterStu
 hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st, const FilterStudy* fs = nullptr);
 // x [n][ld] (fp32 or bf16) -> bf16 [n][d + 16]: rn(scale * x) | split of norms[r] (or 1 1 1) | 0
 hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int ld, int d, const float* norms, float scale,
-                               uint16_t* out, hipStream_t st);
+                               uint16_t* out, hipStream_t st, const int32_t* gate = nullptr);
 // Starting thresholds of the GEMM filter (k_seed_threshold): gthr[q] = ordered k-th
 // smallest exact D from query q to ns <= KNN_SEED_MAX_ROWS rows spread over train.
 #define KNN_SEED_MAX_ROWS 2048

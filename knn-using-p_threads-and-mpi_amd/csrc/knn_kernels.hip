@@ -63,6 +63,40 @@ __device__ __forceinline__ float direct_dist(const float* q, const E* __restrict
     }
     return sum;
 }
+// The same distance with the train row read in batches of 8 independent float4 loads
+// (one memory round trip per 32 features instead of one per 4): for the rescore's
+// scattered survivor rows.  Summation order and roundings are direct_dist's.
+template <typename E>
+__device__ __forceinline__ float direct_dist_batched(const float* q, const E* __restrict__ t, int d) {
+    if ((((uintptr_t)t) & (4 * sizeof(E) - 1)) != 0) return direct_dist(q, t, d);
+    float sum = 0.0f;
+    int i = 0;
+    for (; i + 32 <= d; i += 32) {
+        float4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = load4(t + i + 4 * j);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int b = i + 4 * j;
+            float d0 = q[b + 0] - v[j].x; sum = sum + d0 * d0;
+            float d1 = q[b + 1] - v[j].y; sum = sum + d1 * d1;
+            float d2 = q[b + 2] - v[j].z; sum = sum + d2 * d2;
+            float d3 = q[b + 3] - v[j].w; sum = sum + d3 * d3;
+        }
+    }
+    for (; i + 4 <= d; i += 4) {
+        const float4 v = load4(t + i);
+        float d0 = q[i + 0] - v.x; sum = sum + d0 * d0;
+        float d1 = q[i + 1] - v.y; sum = sum + d1 * d1;
+        float d2 = q[i + 2] - v.z; sum = sum + d2 * d2;
+        float d3 = q[i + 3] - v.w; sum = sum + d3 * d3;
+    }
+    for (; i < d; i++) {
+        float df = q[i] - widen(t[i]);
+        sum = sum + df * df;
+    }
+    return sum;
+}
 #pragma clang fp contract(on)
 
 // ---------------------------------------------------------------------------------
@@ -404,7 +438,8 @@ __global__ __launch_bounds__(256) void k_row_norms(const E* __restrict__ x, int6
                                                    int32_t* __restrict__ status,
                                                    uint32_t* __restrict__ maxo,
                                                    float* __restrict__ outp, float c1,
-                                                   float* __restrict__ tmax) {
+                                                   float* __restrict__ tmax, const int32_t* __restrict__ gate) {
+    if (gate && *gate == 0) return;  // a gated stage (AUTO's re-run) that is not taken
     // rows [n, n + 64) of out/outp get +inf: the GEMM filter's tile tail reads them
     int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
     float s = 0.0f;
@@ -445,7 +480,8 @@ __global__ __launch_bounds__(256) void k_row_norms(const E* __restrict__ x, int6
 // 4 elements (coalesced float4 in, two 8-byte bf16 quads out).
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_split_rows(const float* __restrict__ x, int64_t n, int ld, int d,
-                                                    bf16_t* __restrict__ out) {
+                                                    bf16_t* __restrict__ out, const int32_t* __restrict__ gate) {
+    if (gate && *gate == 0) return;
     const int per_row = d >> 2;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n * per_row) return;
@@ -471,7 +507,8 @@ __global__ __launch_bounds__(256) void k_split_rows(const float* __restrict__ x,
 // elements (coalesced float4 in, one 8-byte bf16 quad out).
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_round_rows(const float* __restrict__ x, int64_t n, int ld, int d,
-                                                    bf16_t* __restrict__ out) {
+                                                    bf16_t* __restrict__ out, const int32_t* __restrict__ gate) {
+    if (gate && *gate == 0) return;
     const int per_row = d >> 2;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n * per_row) return;
@@ -519,7 +556,6 @@ __global__ __launch_bounds__(256) void k_round_rows(const float* __restrict__ x,
 // passes (slow path).  Kept rows go to this segment's slice of the query's candidate
 // list (LDS counter).
 // ---------------------------------------------------------------------------------
-static constexpr int GF_BM1 = 128;  // queries per block per query group
 #ifndef KNN_FILTER_DEFER
 #define KNN_FILTER_DEFER 1  // 8-wave shape: record passing values, flush them every KNN_FILTER_DEFER_EVERY tiles
 #endif
@@ -530,6 +566,7 @@ static constexpr int GF_BM1 = 128;  // queries per block per query group
 
 template <typename E, int RB, int MINW, int NBUF, int NW, int QG, int RG>
 __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a) {
+    if ((a.gate && *a.gate == 0) || (*a.status & KNN_STATUS_GEMM_UNSAFE)) return;  // not taken / exact path
     typedef FilterTile<RB, NW, QG, RG> FT;
     constexpr bool BF = sizeof(E) == 2;
     constexpr bool SPLIT = std::is_same<E, split_t>::value;  // [hi | lo] rows of fp32 data
@@ -1112,11 +1149,17 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 }
 
 // ---------------------------------------------------------------------------------
-// k_rescore<R, CAPW, E>: one wave per query.  Final threshold = k-th smallest U among
-// the query's candidates (found by bisection over ordered float bits); candidates with
-// L <= threshold are rescored with the exact direct form and selected by key.
-// Queries whose list overflowed (or holds < k entries) go to the exact fallback list.
-// LDS per wave: q row [ld_pad] f32 | counts [C] i32 | survivors [64*CAPW] i32
+// k_rescore<R, CAPW, E>: one wave per query.  Final threshold = the k-th smallest U among
+// the query's candidates; candidates with L <= threshold are rescored with the exact
+// direct form and selected by key.  Queries whose list overflowed (or holds < k entries)
+// go to the exact fallback list.
+//  * The candidates sit in a.nseg (<= 16) sub-slices of cap_seg entries; compact entry e
+//    maps to (slice, offset) through the slices' prefix sums.  Their ordered U bits are
+//    staged in LDS (su, <= 64 CAPW words), so the bisection reads only the entries that
+//    exist, in ceil(total / 64) ballots per round, and between the wave's smallest and
+//    largest U instead of over all 2^32 values.
+//  * The survivors (L <= threshold) reuse su as their compact index list.
+// LDS per wave: q row [ld_pad] f32 | counts [C] i32 (C <= KNN_VOTE_LDS_MAX_C) | su [64*CAPW]
 // ---------------------------------------------------------------------------------
 template <int R, int CAPW, typename E>
 __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
@@ -1126,55 +1169,87 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
     unsigned char* my = smem + (size_t)wave * a.wave_lds_bytes;
     float* qs = reinterpret_cast<float*>(my);
     int* counts = a.c_lds_bytes ? reinterpret_cast<int*>(my + a.q_lds_bytes) : nullptr;  // NULL: vote_ballot
-    int32_t* surv = reinterpret_cast<int32_t*>(my + a.q_lds_bytes + a.c_lds_bytes);
+    uint32_t* su = reinterpret_cast<uint32_t*>(my + a.q_lds_bytes + a.c_lds_bytes);
     const int64_t q = (int64_t)blockIdx.x * 4 + wave;
     if (q >= a.nq) return;
+    if (a.gate && *a.gate == 0) return;  // a gated stage (AUTO's re-run) that is not taken
+    if (*a.status & KNN_STATUS_GEMM_UNSAFE) {
+        // a norm too large for the certificate: every query takes the exact scan
+        if (lane == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = (int32_t)q;
+        return;
+    }
     const int k = a.k;
     const E* train = reinterpret_cast<const E*>(a.train);
     const E* test = reinterpret_cast<const E*>(a.test);
-    int total = 0;
-    bool overflow = false;
-    for (int sg = 0; sg < a.nseg; sg++) {
-        const int ns = a.cnt[(int64_t)sg * a.nq + q];
-        overflow |= ns > a.cap_seg;
-        total += ns;
+    // sub-slice fills: lane sg < nseg holds slice sg's; inclusive prefix over lanes 0..15
+    const int cs = lane < a.nseg ? a.cnt[(int64_t)lane * a.nq + q] : 0;
+    const bool overflow = __ballot(cs > a.cap_seg) != 0ull;
+    int incl = cs;
+#pragma unroll
+    for (int j = 1; j < 16; j <<= 1) {
+        const int o = __shfl_up(incl, j);
+        if ((lane & 15) >= j) incl += o;
     }
+    const int total = __shfl(incl, 15);
     if (overflow || total < k) {
         if (lane == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = (int32_t)q;
         return;
     }
-    // load candidates (ordered-uint U, float L); entry e lives in segment e / cap_seg
-    uint32_t uo[CAPW];
-    float lv[CAPW];
-#pragma unroll
-    for (int i = 0; i < CAPW; i++) {
+    const int excl = incl - cs;
+    const int64_t qbase = q * (int64_t)a.cap;
+    // candidate position of compact entry e: slice = last sg with excl[sg] <= e
+    auto position = [&](int e) __attribute__((always_inline)) -> int64_t {
+        int sg = 0, base = 0;
+        for (int s2 = 1; s2 < a.nseg; s2++) {  // uniform loop, <= 15 steps
+            const int ex = __shfl(excl, s2);
+            if (e >= ex) { sg = s2; base = ex; }
+        }
+        return qbase + (int64_t)sg * a.cap_seg + (e - base);
+    };
+    const int nreg = (total + 63) >> 6;  // <= CAPW (total <= nseg * cap_seg <= cap)
+    uint32_t umin = 0xffffffffu, umax = 0u;
+    for (int i = 0; i < nreg; i++) {
         const int e = lane + 64 * i;
-        const int sg = e / a.cap_seg;
-        const bool v = sg < a.nseg && (e - sg * a.cap_seg) < a.cnt[(int64_t)min(sg, a.nseg - 1) * a.nq + q];
-        const int64_t o = q * (int64_t)a.cap + e;
-        uo[i] = v ? f2o(a.cand_U[o]) : 0xffffffffu;
-        lv[i] = v ? a.cand_L[o] : __uint_as_float(0x7f800000u);
+        const int64_t o = position(e);
+        if (e < total) {
+            const uint32_t u = f2o(a.cand_U[o]);
+            su[e] = u;
+            umin = min(umin, u);
+            umax = max(umax, u);
+        }
     }
-    // smallest x with #{U <= x} >= k
-    uint32_t lo = 0u, hi = 0xfffffffeu;
-    while (lo < hi) {
-        uint32_t mid = lo + ((hi - lo) >> 1);
-        int c = 0;
 #pragma unroll
-        for (int i = 0; i < CAPW; i++) c += __popcll(__ballot(uo[i] <= mid));
+    for (int j = 32; j > 0; j >>= 1) {
+        umin = min(umin, (uint32_t)__shfl_xor((int)umin, j));
+        umax = max(umax, (uint32_t)__shfl_xor((int)umax, j));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // the threshold: the smallest x with #{U <= x} >= k, or any x above it -- every x >= it
+    // is a valid bound (it only admits more survivors) -- so the bisection stops at 2^10
+    // ordered-float steps (2^-13 relative), far inside the certificate's band
+    uint32_t lo = umin, hi = umax;
+    while (hi - lo > 1024u) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        int c = 0;
+        for (int i = 0; i < nreg; i++) {
+            const int e = lane + 64 * i;
+            c += __popcll(__ballot(e < total && su[e] <= mid));
+        }
         if (c >= k) hi = mid; else lo = mid + 1;
     }
-    const float thr = o2f(lo);
-    // compact survivors L <= thr
+    const float thr = o2f(hi);
+    // compact survivors L <= thr into su (a write never overtakes an unread entry)
     int m = 0;
-#pragma unroll
-    for (int i = 0; i < CAPW; i++) {
-        bool s = lv[i] <= thr && uo[i] != 0xffffffffu;
-        u64 bal = __ballot(s);
-        if (s) {
-            int pos = m + __popcll(bal & ((1ull << lane) - 1ull));
-            surv[pos] = a.cand_idx[q * (int64_t)a.cap + lane + 64 * i];
-        }
+    for (int i = 0; i < nreg; i++) {
+        const int e = lane + 64 * i;
+        const int64_t o = position(e);
+        const bool sv = e < total && a.cand_L[o] <= thr;
+        const int32_t t = sv ? a.cand_idx[o] : 0;
+        const u64 bal = __ballot(sv);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (sv) su[m + __popcll(bal & ((1ull << lane) - 1ull))] = (uint32_t)t;
         m += __popcll(bal);
     }
     for (int i = lane; i < a.d; i += 64) qs[i] = widen(test[q * a.ld_q + i]);
@@ -1188,10 +1263,10 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
     for (int b = 0; b < m; b += 64) {
         u64 key = KEY_NONE;
         if (b + lane < m) {
-            int32_t t = surv[b + lane];
-            key = make_key(direct_dist(qs, train + (int64_t)t * a.ld_t, a.d), (uint32_t)t);
+            const int32_t t = (int32_t)su[b + lane];
+            key = make_key(direct_dist_batched(qs, train + (int64_t)t * a.ld_t, a.d), (uint32_t)t);
         }
-        bool pass = key < kth;
+        const bool pass = key < kth;
         if (__ballot(pass)) {
             topk_merge<R>(T, pass ? key : KEY_NONE);
             kth = list_at(T, k - 1);
@@ -1408,6 +1483,41 @@ __global__ __launch_bounds__(256) void k_confusion(const int32_t* __restrict__ p
 }
 
 // ---------------------------------------------------------------------------------
+// Device-side control of a predict call (no host round trip inside a call):
+//   k_fill_u32     p[0..n) = v when the gate is open (a gated stage's threshold reset)
+//   k_rerun_decide AUTO's re-run of the rounded filter as split: open the gate when the
+//                  call is not on the exact path and more than `limit` queries fell back,
+//                  and reset the fallback list the split run rebuilds
+// ctrl: [0] status bits, [1] fallback count, [2] ordered max train norm, [3] re-run gate
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fill_u32(uint32_t* __restrict__ p, int64_t n, uint32_t v,
+                                                  const int32_t* __restrict__ gate) {
+    if (gate && *gate == 0) return;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = v;
+}
+
+__global__ void k_rerun_decide(int32_t* ctrl, int64_t limit) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int open = !(ctrl[0] & KNN_STATUS_GEMM_UNSAFE) && (int64_t)ctrl[1] > limit;
+    ctrl[3] = open;
+    if (open) ctrl[1] = 0;
+}
+
+hipError_t knn_launch_fill_u32(uint32_t* p, int64_t n, uint32_t v, const int32_t* gate, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_fill_u32, dim3(grid), dim3(256), 0, st, p, n, v, gate);
+    KNN_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t knn_launch_rerun_decide(int32_t* ctrl, int64_t limit, hipStream_t st) {
+    hipLaunchKernelGGL(k_rerun_decide, dim3(1), dim3(64), 0, st, ctrl, limit);
+    KNN_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------------
 // Launchers (host side)
 // ---------------------------------------------------------------------------------
 static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -1506,16 +1616,16 @@ hipError_t knn_launch_direct_tile(DirectTileArgs a, hipStream_t st) {
 
 hipError_t knn_launch_row_norms(const void* x, int elem, int64_t n, int ld, int d, float* out,
                                 int32_t* status, uint32_t* maxo, float* outp, float c1, hipStream_t st,
-                                float* tmax) {
+                                float* tmax, const int32_t* gate) {
     if (n <= 0) return hipSuccess;
     const int64_t rows = n + (outp ? 64 : 0);
     dim3 grid((unsigned)((rows + 255) / 256));
     if (elem == ELEM_BF16)
         hipLaunchKernelGGL(k_row_norms<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, n, ld, d, out,
-                           status, maxo, outp, c1, tmax);
+                           status, maxo, outp, c1, tmax, gate);
     else
         hipLaunchKernelGGL(k_row_norms<float>, grid, dim3(256), 0, st, (const float*)x, n, ld, d, out,
-                           status, maxo, outp, c1, tmax);
+                           status, maxo, outp, c1, tmax, gate);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -1758,20 +1868,22 @@ hipError_t knn_launch_confusion(const int32_t* pred, const int32_t* labels, int6
     return hipSuccess;
 }
 
-hipError_t knn_launch_split_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st) {
+hipError_t knn_launch_split_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st,
+                                 const int32_t* gate) {
     const int64_t total = n * (d / 4);
     if (total <= 0) return hipSuccess;
     if (d % 4 || ld % 4) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_split_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, n, ld, d, out);
+    hipLaunchKernelGGL(k_split_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, n, ld, d, out, gate);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }
 
-hipError_t knn_launch_round_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st) {
+hipError_t knn_launch_round_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st,
+                                 const int32_t* gate) {
     const int64_t total = n * (d / 4);
     if (total <= 0) return hipSuccess;
     if (d % 4 || ld % 4) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_round_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, n, ld, d, out);
+    hipLaunchKernelGGL(k_round_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, n, ld, d, out, gate);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -24,7 +24,7 @@ def test_library_exports_every_header_symbol(knn):
     assert len(syms) >= 14
     for s in syms:
         assert hasattr(lib, s), s
-    assert lib.knn_version() == 1
+    assert lib.knn_version() == 2
 
 
 def test_cpp_surface_symbols_exported():

@@ -193,6 +193,30 @@ def test_auto_rounded_filter_rerun(knn, oracle, ctxs, case):
     assert np.array_equal(pred, dpred)
 
 
+@pytest.mark.parametrize("algo", ["gemm", "gemm_split", "gemm_bf16", "auto"])
+def test_gemm_norm_guard(knn, oracle, ctxs, algo):
+    """Rows whose squared norm reaches 2^125 are outside the GEMM certificate: the filter
+    skips on the device (status bit) and every query takes the exact fallback scan --
+    same results, and no host round trip inside the call."""
+    rng = np.random.default_rng(51)
+    nt, nq, d = 20000, 70, 64
+    tr = rng.standard_normal((nt, d)).astype(np.float32)
+    te = rng.standard_normal((nq, d)).astype(np.float32)
+    tr[123] *= np.float32(2.0 ** 62)  # ||t||^2 ~ 2^130
+    tl = rng.integers(0, 10, size=nt).astype(np.int32)
+    if algo == "auto":
+        tr = np.tile(tr, (3, 1))[: 3 * nt]   # nt * nq >= 1e9 is not needed: AUTO picks by size,
+        tl = np.tile(tl, 3)                 # so force the GEMM path through the filter algos
+    for k in (1, 10):
+        bad, opred, odist, oidx = oracle.knn(tr, tl, te, k, 10)
+        assert bad == 0
+        pred, dist, idx = ctxs[algo].predict(tr, tl, te, k, 10, topk=True)
+        assert np.array_equal(idx, oidx) and np.array_equal(pred, opred), (algo, k)
+        assert np.array_equal(dist.view(np.uint32), odist.view(np.uint32)), (algo, k)
+        if algo != "auto":
+            assert ctxs[algo].stats()["fallback_queries"] == nq
+
+
 def test_edge_cases(knn, ctxs):
     tr = np.arange(12, dtype=np.float32).reshape(6, 2)
     tl = np.array([0, 1, 2, 1, 0, 1], np.int32)
