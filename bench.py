@@ -63,20 +63,48 @@ FILTER_ROOF = {"f32": (157.3, 1), "bf16": (2500.0, 1), "bf16x3 split": (2500.0 /
 PMC_SUFFIX = {"bf16x3 split": "/split", "bf16 rounded": "/bf16r"}
 
 
+MPIEXEC = os.environ.get("KNN_MPIEXEC", "/opt/conda/bin/mpiexec")
+
+
+def _ref_exe(name):
+    return os.path.join(REPO, "oracle", "_ref", name)
+
+
 def cpu_baseline(d, k, C, seed, kind=0):
-    """Reference pthreads KNN (multi-thread.cpp:37) on a bounded sample of the workload."""
+    """Reference pthreads KNN (multi-thread.cpp:37) on a bounded sample of the workload,
+    beside it the same sample through the reference's -O2 build (ref_bench_O2) and the
+    reference's MPI path (mpi.cpp:141-186, ref_bench_mpi under mpiexec, as many ranks as
+    threads)."""
     threads = int(os.environ.get("KNN_BENCH_CPU_THREADS", min(16, os.cpu_count() or 1)))
     # ~1e8 pairs at d=128 (10-30 s of CPU work at -O0); fewer train rows at larger d
     nt_s, nq_s = 100_000 * 128 // max(d, 128), 64 * threads
-    exe = os.path.join(REPO, "oracle", "_ref", "ref_bench")
+    exe = _ref_exe("ref_bench")
     sample = f"{nq_s} queries x {nt_s} train rows (d={d}, k={k}) of the same generator"
+    argv = [str(kind), str(seed), str(nt_s), str(nq_s), str(d), str(k), str(C)]
+
+    def run(cmd):
+        out = subprocess.run(cmd, capture_output=True, text=True, check=True, timeout=600)
+        return json.loads(out.stdout.strip().splitlines()[-1])
+
     if os.path.exists(exe):
-        out = subprocess.run([exe, str(kind), str(seed), str(nt_s), str(nq_s), str(d), str(k), str(C),
-                              str(threads)], capture_output=True, text=True, check=True, timeout=600)
-        r = json.loads(out.stdout.strip().splitlines()[-1])
-        return {"value": r["pairs_per_s"], "unit": "pairs/s", "cores": threads, "kind": "reference",
-                "sample": sample + "; reference multi-thread.cpp KNN built -O0 as shipped",
-                "queries_per_s": r["queries_per_s"]}
+        r = run([exe] + argv + [str(threads)])
+        rec = {"value": r["pairs_per_s"], "unit": "pairs/s", "cores": threads, "kind": "reference",
+               "sample": sample + "; reference multi-thread.cpp KNN built -O0 as shipped",
+               "queries_per_s": r["queries_per_s"]}
+        if os.path.exists(_ref_exe("ref_bench_O2")):
+            r2 = run([_ref_exe("ref_bench_O2")] + argv + [str(threads)])
+            rec["O2"] = {"value": r2["pairs_per_s"], "unit": "pairs/s", "cores": threads,
+                         "queries_per_s": r2["queries_per_s"],
+                         "note": "the same sample through multi-thread.cpp built -O2"}
+        if os.path.exists(_ref_exe("ref_bench_mpi")) and os.path.exists(MPIEXEC):
+            r3 = run([MPIEXEC, "-n", str(threads), _ref_exe("ref_bench_mpi")] + argv)
+            rec["mpi"] = {"value": r3["pairs_per_s"], "unit": "pairs/s", "cores": threads,
+                          "queries_per_s": r3["queries_per_s"],
+                          "note": f"the same sample through mpi.cpp's KNN + Scatter/Gatherv, -O0, MPICH, "
+                                  f"mpiexec -n {threads}"}
+        else:
+            rec["mpi"] = "absent"
+        return rec
     # fallback: the C restatement (same algorithm, -O2), labelled as a port
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from conftest import Oracle
@@ -87,7 +115,7 @@ def cpu_baseline(d, k, C, seed, kind=0):
     o.knn(tr, tl, te, k, C, threads=threads, topk=False)
     dt = time.perf_counter() - t0
     return {"value": nt_s * nq_s / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": sample + "; oracle/knn_oracle.c -O2", "queries_per_s": nq_s / dt}
+            "sample": sample + "; oracle/knn_oracle.c -O2", "queries_per_s": nq_s / dt, "mpi": "absent"}
 
 
 def cpu_baseline_arff(k, threads=None):
@@ -109,10 +137,17 @@ def cpu_baseline_arff(k, threads=None):
     mt = sorted(run([exe_mt, tr, te, str(k), str(threads)]) for _ in range(3))[1]
     se = run([exe_se, tr, te, str(k)])
     pairs = 30_803 * 1_718
-    return {"value": pairs / (mt * 1e-3), "unit": "pairs/s", "cores": threads, "kind": "reference",
-            "sample": f"the whole workload (large ARFF pair, k={k}); reference multi-thread.cpp with "
-                      f"{threads} threads, -O0 as shipped, median of 3 (ms resolution)",
-            "ms": mt, "serial_main_ms": se, "serial_main_pairs_per_s": pairs / (se * 1e-3)}
+    rec = {"value": pairs / (mt * 1e-3), "unit": "pairs/s", "cores": threads, "kind": "reference",
+           "sample": f"the whole workload (large ARFF pair, k={k}); reference multi-thread.cpp with "
+                     f"{threads} threads, -O0 as shipped, median of 3 (ms resolution)",
+           "ms": mt, "serial_main_ms": se, "serial_main_pairs_per_s": pairs / (se * 1e-3)}
+    if os.path.exists(_ref_exe("mpi")) and os.path.exists(MPIEXEC):
+        mp = sorted(run([MPIEXEC, "-n", str(threads), _ref_exe("mpi"), tr, te, str(k)]) for _ in range(3))[1]
+        rec["mpi"] = {"value": pairs / (mp * 1e-3), "unit": "pairs/s", "cores": threads, "ms": mp,
+                      "note": f"reference mpi.cpp (-O0, MPICH), mpiexec -n {threads}, median of 3"}
+    else:
+        rec["mpi"] = "absent"
+    return rec
 
 
 def bench_arff(args, knn, torch, local):

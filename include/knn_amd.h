@@ -38,7 +38,8 @@ typedef enum {
     KNN_EHIP = 3,     /* a HIP runtime call failed */
     KNN_ERANGE = 4,   /* fewer than k neighbours with a finite distance (< FLT_MAX) */
     KNN_ENODEV = 5,   /* no usable gfx950 device */
-    KNN_EIO = 6       /* file could not be opened / parsed (ARFF loader) */
+    KNN_EIO = 6,      /* file could not be opened / parsed (ARFF loader) */
+    KNN_ERCCL = 7     /* an RCCL call failed (train-sharded exchange) */
 } knn_status;
 
 typedef enum { KNN_F32 = 0, KNN_BF16 = 1 } knn_dtype;
@@ -92,8 +93,15 @@ typedef struct knn_ctx knn_ctx;
 /* Library / ABI version (KNN_AMD_ABI_VERSION). */
 int32_t knn_version(void);
 
+/* Source hash of the tree this library was built from (16 hex digits; computed by
+ * knn-using-p_threads-and-mpi_amd/build_id.py over the package's Makefile, csrc/ and
+ * include/).  Tests compare it with the sources beside the library they load. */
+const char* knn_build_id(void);
+
 /* Create / destroy a context (replaces the per-run setup in main.cpp:114-131,
- * multi-thread.cpp:133-160 and mpi.cpp:119-149). */
+ * multi-thread.cpp:133-160 and mpi.cpp:119-149).  A context serves one call at a time:
+ * threads that share one serialise their calls (the C++ KNN() does, per device), or each
+ * creates its own. */
 knn_status knn_create(knn_ctx** out, const knn_opts* opts);
 void knn_destroy(knn_ctx* ctx);
 
@@ -164,6 +172,38 @@ knn_status knn_shard_topk_device(knn_ctx* ctx, const knn_dataset* train_shard, c
 knn_status knn_merge_vote_device(knn_ctx* ctx, int32_t nsrc, int64_t nq, int32_t k, int32_t num_classes,
                                  const int32_t* d_rec, int32_t* d_pred, float* d_dist, int32_t* d_idx,
                                  void* hip_stream);
+
+/*
+ * Train-sharded KNN over ranks, one process per GPU (replaces the MPI
+ * collective pattern of mpi.cpp:130-201 -- MPI_Init / Scatter / Gatherv -- for a train set
+ * sharded instead of replicated).  The communicator is RCCL (over xGMI on one node),
+ * loaded at knn_comm_create.
+ *   knn_comm_unique_id: 128 opaque bytes made on one rank and handed to every rank by the
+ *     caller's own bootstrap (MPI_Bcast, torch.distributed, a file).
+ *   knn_comm_create: ncclCommInitRank on ctx's device; collective over the nranks ranks.
+ *   knn_predict_train_sharded: rank r holds train rows [idx_base, idx_base + shard->n) and
+ *     every query (test, device buffers); it computes its shard's exact top-k of every query
+ *     (knn_shard_topk_device), one grouped send/recv all-to-all hands each rank the lists of
+ *     the queries it owns, shard_range(test->n, nranks, rank), and k_merge_vote merges them
+ *     by (distance, global index) -- the reference's lower-index tie rule over the whole
+ *     train set -- and votes.  d_pred (and optional d_dist / d_idx [owned][k]) receive the
+ *     owned queries' results.  Collective: every rank calls it with the same test set and k.
+ *   knn_shard_range: the reference's contiguous split with the remainder on the last worker
+ *     (multi-thread.cpp:154-158, mpi.cpp:141-170).
+ *   knn_exchange_layout: element offsets / counts of the all-to-all for `rank` (int32
+ *     records [nq][3][k] sent, [world][owned][3][k] received); arrays of `world` entries.
+ */
+#define KNN_COMM_ID_BYTES 128
+typedef struct knn_comm knn_comm;
+knn_status knn_comm_unique_id(void* id_out);
+knn_status knn_comm_create(knn_ctx* ctx, const void* id, int32_t nranks, int32_t rank, knn_comm** out);
+void knn_comm_destroy(knn_comm* comm);
+knn_status knn_predict_train_sharded(knn_ctx* ctx, knn_comm* comm, const knn_dataset* train_shard, int64_t idx_base,
+                                     const knn_dataset* test, int32_t k, int32_t num_classes, int32_t* d_pred,
+                                     float* d_dist, int32_t* d_idx, void* hip_stream);
+knn_status knn_shard_range(int64_t n, int32_t world, int32_t rank, int64_t* begin, int64_t* end);
+knn_status knn_exchange_layout(int64_t nq, int32_t k, int32_t world, int32_t rank, int64_t* send_off,
+                               int64_t* send_cnt, int64_t* recv_off, int64_t* recv_cnt);
 
 /* Per-stage device times (ms) of the last predict call when opts.profile = 1.
  * names: optional array of n const char* to receive stage names. Returns the

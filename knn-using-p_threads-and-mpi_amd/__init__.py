@@ -28,9 +28,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # KNN_AMD_LIB overrides the library (A/B runs of alternative builds)
 LIB_PATH = os.environ.get("KNN_AMD_LIB") or os.path.join(_HERE, "libknn_amd.so")
 
-KNN_OK, KNN_EINVAL, KNN_ENOMEM, KNN_EHIP, KNN_ERANGE, KNN_ENODEV, KNN_EIO = range(7)
+KNN_OK, KNN_EINVAL, KNN_ENOMEM, KNN_EHIP, KNN_ERANGE, KNN_ENODEV, KNN_EIO, KNN_ERCCL = range(8)
 STATUS_NAMES = {0: "KNN_OK", 1: "KNN_EINVAL", 2: "KNN_ENOMEM", 3: "KNN_EHIP", 4: "KNN_ERANGE",
-                5: "KNN_ENODEV", 6: "KNN_EIO"}
+                5: "KNN_ENODEV", 6: "KNN_EIO", 7: "KNN_ERCCL"}
+KNN_COMM_ID_BYTES = 128
 KNN_F32, KNN_BF16 = 0, 1
 ALGOS = {"auto": 0, "direct": 1, "gemm": 2, "gemm_split": 3, "gemm_bf16": 4, "direct_scan": 5}
 FILTER_OPERANDS = {-1: None, 0: "f32", 1: "bf16", 2: "bf16x3 split", 3: "bf16 rounded"}
@@ -79,6 +80,7 @@ def load_library(path=LIB_PATH):
     DS = ctypes.POINTER(knn_dataset)
     sig = {
         "knn_version": (I32, []),
+        "knn_build_id": (ctypes.c_char_p, []),
         "knn_create": (I32, [ctypes.POINTER(P), ctypes.POINTER(knn_opts)]),
         "knn_destroy": (None, [P]),
         "knn_last_error": (ctypes.c_char_p, [P]),
@@ -92,6 +94,12 @@ def load_library(path=LIB_PATH):
                                ctypes.c_uint32, I32, P]),
         "knn_mfma_probe_bf16": (I32, [P, P, P, I32, P, P]),
         "knn_set_generation": (I32, [P, ctypes.c_uint64]),
+        "knn_comm_unique_id": (I32, [P]),
+        "knn_comm_create": (I32, [P, P, I32, I32, ctypes.POINTER(P)]),
+        "knn_comm_destroy": (None, [P]),
+        "knn_predict_train_sharded": (I32, [P, P, DS, I64, DS, I32, I32, P, P, P, P]),
+        "knn_shard_range": (I32, [I64, I32, I32, ctypes.POINTER(I64), ctypes.POINTER(I64)]),
+        "knn_exchange_layout": (I32, [I64, I32, I32, I32, P, P, P, P]),
         "knn_alloc_pinned": (I32, [ctypes.c_size_t, ctypes.POINTER(P)]),
         "knn_free_pinned": (None, [P]),
         "knn_confusion_matrix": (I32, [P, P, I64, I32, P]),
@@ -409,6 +417,89 @@ class Context:
         return {"candidates": v[0], "fallback_queries": v[1], "train_segments": v[2],
                 "filter_operands": FILTER_OPERANDS.get(v[3], v[3]), "rerun_split": bool(v[4]),
                 "fused_norm": bool(v[5]), "h2d_train_bytes": v[6], "h2d_query_bytes": v[7]}
+
+
+def comm_unique_id():
+    """knn_comm_unique_id: 128 bytes to hand to every rank (the caller's bootstrap)."""
+    lib = load_library()
+    buf = ctypes.create_string_buffer(KNN_COMM_ID_BYTES)
+    st = lib.knn_comm_unique_id(buf)
+    if st != KNN_OK:
+        raise KnnError(st, "knn_comm_unique_id")
+    return buf.raw
+
+
+def build_id():
+    """(id baked into the loaded libknn_amd.so, id of the sources beside it): equal when the
+    library was built from this tree (build_id.py)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("knn_amd_build_id", os.path.join(_HERE, "build_id.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return load_library().knn_build_id().decode(), mod.compute()
+
+
+def shard_range_c(n, world, rank):
+    """knn_shard_range (the C ABI's copy of shard_range, used by knn_predict_train_sharded)."""
+    lib = load_library()
+    a, b = ctypes.c_int64(), ctypes.c_int64()
+    st = lib.knn_shard_range(n, world, rank, ctypes.byref(a), ctypes.byref(b))
+    if st != KNN_OK:
+        raise KnnError(st, "knn_shard_range")
+    return a.value, b.value
+
+
+def exchange_layout(nq, k, world, rank):
+    """knn_exchange_layout: (send_off, send_cnt, recv_off, recv_cnt) int32-element arrays of
+    the train-sharded all-to-all of rank `rank`."""
+    lib = load_library()
+    arrs = [np.zeros(world, np.int64) for _ in range(4)]
+    st = lib.knn_exchange_layout(nq, k, world, rank, *[_ptr(a) for a in arrs])
+    if st != KNN_OK:
+        raise KnnError(st, "knn_exchange_layout")
+    return tuple(arrs)
+
+
+class Comm:
+    """An RCCL communicator bound to a context (knn_comm_create; collective over nranks)."""
+
+    def __init__(self, ctx, uid, nranks, rank):
+        self.lib = ctx.lib
+        self.ctx = ctx
+        self.nranks, self.rank = nranks, rank
+        h = ctypes.c_void_p()
+        st = self.lib.knn_comm_create(ctx.h, ctypes.create_string_buffer(bytes(uid), KNN_COMM_ID_BYTES), nranks,
+                                      rank, ctypes.byref(h))
+        if st != KNN_OK:
+            raise KnnError(st, f"knn_comm_create(nranks={nranks}, rank={rank})")
+        self.h = h
+
+    def predict_train_sharded(self, shard, labels, idx_base, test, k, num_classes, pred, dist=None, idx=None,
+                              stream=None, d=None):
+        """knn_predict_train_sharded: this rank's train shard (global rows [idx_base, ...)) and
+        every query in, the owned queries' (shard_range) predictions out."""
+        tr = _device_dataset(shard, labels, d)
+        te = _device_dataset(test, None, d)
+        q0, q1 = shard_range(te.n, self.nranks, self.rank)
+        _outputs(q1 - q0, k, pred, dist, idx)
+        st = self.lib.knn_predict_train_sharded(
+            self.ctx.h, self.h, ctypes.byref(tr), idx_base, ctypes.byref(te), k, num_classes, pred.data_ptr(),
+            None if dist is None else dist.data_ptr(), None if idx is None else idx.data_ptr(),
+            None if stream is None else ctypes.c_void_p(stream))
+        if st != KNN_OK:
+            raise KnnError(st, self.lib.knn_last_error(self.ctx.h).decode())
+        return q0, q1
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.knn_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class PinnedArray:

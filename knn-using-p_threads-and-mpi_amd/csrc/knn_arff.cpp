@@ -363,6 +363,10 @@ void flatten(const ParsedArff& P, KnnFlatView* out) {
 // ---------------------------------------------------------------------------------
 struct Devices {
     std::vector<knn_ctx*> ctx;
+    // a knn_ctx serves one call at a time: the reference's pthreads driver calls KNN from
+    // numThreads threads at once (multi-thread.cpp:170-192), so calls that land on the same
+    // device queue here (the device runs them back to back either way)
+    std::vector<std::unique_ptr<std::mutex>> busy;
     std::mutex mu;
 };
 Devices& devices() {
@@ -384,6 +388,7 @@ std::vector<knn_ctx*>& contexts() {
                 break;
             }
             D.ctx.push_back(c);
+            D.busy.emplace_back(new std::mutex());
         }
     }
     return D.ctx;
@@ -413,7 +418,10 @@ void predict_range(ArffData* train, ArffData* test, int k, int64_t q0, int64_t q
     for (int g = 0; g < G; g++) {
         const int64_t e = s + per + (g == G - 1 ? left : 0);
         int32_t* dst = reinterpret_cast<int32_t*>(out) + (s - q0);
-        auto job = [&, g, s, e, dst]() { st[g] = knn_predict(cs[g], &dtr, &dte, k, C, s, e, dst, nullptr, nullptr); };
+        auto job = [&, g, s, e, dst]() {
+            std::lock_guard<std::mutex> busy(*devices().busy[g]);
+            st[g] = knn_predict(cs[g], &dtr, &dte, k, C, s, e, dst, nullptr, nullptr);
+        };
         if (G == 1) job(); else th.emplace_back(job);
         s = e;
     }

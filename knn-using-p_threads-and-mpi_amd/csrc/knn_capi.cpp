@@ -603,6 +603,9 @@ const char* knn_last_error(const knn_ctx* c) { return c ? c->err.c_str() : "null
 
 }  // extern "C"
 
+int knn_ctx_device(const knn_ctx* c) { return c->device; }
+void* knn_ctx_stream(const knn_ctx* c) { return (void*)c->stream; }
+
 namespace {
 
 // Validation shared by the device entry points.

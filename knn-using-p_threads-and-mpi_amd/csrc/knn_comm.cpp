@@ -1,0 +1,223 @@
+// knn_comm.cpp -- train-sharded KNN over ranks behind the C ABI: an RCCL
+// communicator (one process per GPU, xGMI on one node) and the exchange of per-shard
+// neighbour lists.
+//
+// The reference shards only the test set (mpi.cpp:141-186: MPI_Scatter of [start, end)
+// ranges, MPI_Gatherv of int predictions).  Here a rank may own a contiguous shard of the
+// TRAIN set instead (config C: 32M rows do not need to be replicated): every rank computes
+// its shard's exact top-k for every query (knn_shard_topk_device), one grouped
+// ncclSend/ncclRecv all-to-all hands rank b the lists of the queries it owns
+// (shard_range(nq, world, b), the reference's split), and k_merge_vote merges them by
+// (distance, global index) -- the reference's lower-index tie rule over the whole train
+// set -- and votes.
+//
+// RCCL is loaded with dlopen when the first communicator is created: the library has no
+// link-time dependency on it, and a process that already holds an RCCL (PyTorch's, same
+// SONAME librccl.so.1) shares that one.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/knn_amd.h"
+
+// context accessors (knn_capi.cpp)
+int knn_ctx_device(const knn_ctx* c);
+void* knn_ctx_stream(const knn_ctx* c);
+
+namespace {
+
+struct Rccl {
+    void* h = nullptr;
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    std::string err;
+};
+
+Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"}) {
+            r.h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+            if (r.h) break;
+        }
+        if (!r.h) {
+            r.err = std::string("RCCL not found: ") + dlerror();
+            return;
+        }
+#define KNN_RCCL_SYM(field, sym) r.field = reinterpret_cast<decltype(r.field)>(dlsym(r.h, sym))
+        KNN_RCCL_SYM(get_unique_id, "ncclGetUniqueId");
+        KNN_RCCL_SYM(init_rank, "ncclCommInitRank");
+        KNN_RCCL_SYM(destroy, "ncclCommDestroy");
+        KNN_RCCL_SYM(group_start, "ncclGroupStart");
+        KNN_RCCL_SYM(group_end, "ncclGroupEnd");
+        KNN_RCCL_SYM(send, "ncclSend");
+        KNN_RCCL_SYM(recv, "ncclRecv");
+        KNN_RCCL_SYM(error_string, "ncclGetErrorString");
+#undef KNN_RCCL_SYM
+        if (!r.get_unique_id || !r.init_rank || !r.destroy || !r.group_start || !r.group_end || !r.send || !r.recv)
+            r.err = "RCCL lacks a required symbol";
+    });
+    return r;
+}
+
+bool rccl_ok() {
+    Rccl& r = rccl();
+    return r.h && r.err.empty();
+}
+
+}  // namespace
+
+struct knn_comm {
+    ncclComm_t comm = nullptr;
+    int32_t nranks = 0, rank = 0, device = 0;
+    // exchange workspace: this rank's shard records for all queries, and the lists of its
+    // owned queries from every rank
+    void* rec = nullptr;
+    size_t rec_bytes = 0;
+    void* lists = nullptr;
+    size_t lists_bytes = 0;
+    std::string err;
+};
+
+namespace {
+
+hipError_t grow(void** p, size_t* have, size_t need) {
+    if (*p && *have >= need) return hipSuccess;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+    hipError_t e = hipMalloc(p, need ? need : 16);
+    if (e == hipSuccess) *have = need;
+    return e;
+}
+
+}  // namespace
+
+extern "C" {
+
+knn_status knn_shard_range(int64_t n, int32_t world, int32_t rank, int64_t* begin, int64_t* end) {
+    if (n < 0 || world < 1 || rank < 0 || rank >= world || !begin || !end) return KNN_EINVAL;
+    // multi-thread.cpp:154-158 / mpi.cpp:141-170: worker w < world-1 gets [w*(n/world),
+    // (w+1)*(n/world)); the last worker also takes the remainder
+    const int64_t per = n / world;
+    *begin = (int64_t)rank * per;
+    *end = *begin + per + (rank == world - 1 ? n % world : 0);
+    return KNN_OK;
+}
+
+knn_status knn_exchange_layout(int64_t nq, int32_t k, int32_t world, int32_t rank, int64_t* send_off,
+                               int64_t* send_cnt, int64_t* recv_off, int64_t* recv_cnt) {
+    if (nq < 0 || k < 1 || world < 1 || rank < 0 || rank >= world || !send_off || !send_cnt || !recv_off || !recv_cnt)
+        return KNN_EINVAL;
+    // records are int32 [nq][3][k]; rank b owns queries shard_range(nq, world, b): it receives
+    // from every rank a the rows of its own queries, into lists [a][my_nq][3][k]
+    const int64_t row = 3 * (int64_t)k;
+    int64_t m0, m1;
+    knn_shard_range(nq, world, rank, &m0, &m1);
+    for (int32_t b = 0; b < world; b++) {
+        int64_t b0, b1;
+        knn_shard_range(nq, world, b, &b0, &b1);
+        send_off[b] = b0 * row;
+        send_cnt[b] = (b1 - b0) * row;
+        recv_off[b] = (int64_t)b * (m1 - m0) * row;
+        recv_cnt[b] = (m1 - m0) * row;
+    }
+    return KNN_OK;
+}
+
+knn_status knn_comm_unique_id(void* id_out) {
+    if (!id_out) return KNN_EINVAL;
+    if (!rccl_ok()) return KNN_ENODEV;
+    ncclUniqueId id;
+    if (rccl().get_unique_id(&id) != ncclSuccess) return KNN_ERCCL;
+    std::memcpy(id_out, &id, sizeof(id));
+    return KNN_OK;
+}
+
+knn_status knn_comm_create(knn_ctx* ctx, const void* id, int32_t nranks, int32_t rank, knn_comm** out) {
+    if (!ctx || !id || !out || nranks < 1 || rank < 0 || rank >= nranks) return KNN_EINVAL;
+    *out = nullptr;
+    if (!rccl_ok()) return KNN_ENODEV;
+    knn_comm* c = new (std::nothrow) knn_comm();
+    if (!c) return KNN_ENOMEM;
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = knn_ctx_device(ctx);
+    if (hipSetDevice(c->device) != hipSuccess) {
+        delete c;
+        return KNN_EHIP;
+    }
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    if (rccl().init_rank(&c->comm, nranks, uid, rank) != ncclSuccess) {
+        delete c;
+        return KNN_ERCCL;
+    }
+    *out = c;
+    return KNN_OK;
+}
+
+void knn_comm_destroy(knn_comm* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->comm && rccl_ok()) (void)rccl().destroy(c->comm);
+    if (c->rec) (void)hipFree(c->rec);
+    if (c->lists) (void)hipFree(c->lists);
+    delete c;
+}
+
+knn_status knn_predict_train_sharded(knn_ctx* ctx, knn_comm* comm, const knn_dataset* shard, int64_t idx_base,
+                                     const knn_dataset* test, int32_t k, int32_t num_classes, int32_t* d_pred,
+                                     float* d_dist, int32_t* d_idx, void* hip_stream) {
+    if (!ctx || !comm || !shard || !test) return KNN_EINVAL;
+    if (k < 1 || k > 1024) return KNN_EINVAL;
+    const int64_t nq = test->n;
+    int64_t m0, m1;
+    knn_shard_range(nq, comm->nranks, comm->rank, &m0, &m1);
+    if (m1 > m0 && !d_pred) return KNN_EINVAL;
+    if (hipSetDevice(comm->device) != hipSuccess) return KNN_EHIP;
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : (hipStream_t)knn_ctx_stream(ctx);
+    const size_t row = 3 * (size_t)k * sizeof(int32_t);
+    if (grow(&comm->rec, &comm->rec_bytes, row * (size_t)std::max<int64_t>(nq, 1)) != hipSuccess) return KNN_ENOMEM;
+    if (grow(&comm->lists, &comm->lists_bytes, row * (size_t)std::max<int64_t>(m1 - m0, 1) * comm->nranks) != hipSuccess)
+        return KNN_ENOMEM;
+    // 1. this rank's shard: exact top-k of every query, records with global indices
+    knn_status s = knn_shard_topk_device(ctx, shard, test, k, num_classes, idx_base, (int32_t*)comm->rec, st);
+    if (s != KNN_OK) return s;
+    // 2. all-to-all of the records: rank b receives the rows of its own queries from everyone
+    int64_t so[1024], sc[1024], ro[1024], rc[1024];
+    if (comm->nranks > 1024) return KNN_EINVAL;
+    knn_exchange_layout(nq, k, comm->nranks, comm->rank, so, sc, ro, rc);
+    Rccl& r = rccl();
+    if (r.group_start() != ncclSuccess) return KNN_ERCCL;
+    for (int32_t b = 0; b < comm->nranks; b++) {
+        if (sc[b] > 0 && r.send((const int32_t*)comm->rec + so[b], (size_t)sc[b], ncclInt32, b, comm->comm, st) != ncclSuccess) {
+            r.group_end();
+            return KNN_ERCCL;
+        }
+        if (rc[b] > 0 && r.recv((int32_t*)comm->lists + ro[b], (size_t)rc[b], ncclInt32, b, comm->comm, st) != ncclSuccess) {
+            r.group_end();
+            return KNN_ERCCL;
+        }
+    }
+    if (r.group_end() != ncclSuccess) return KNN_ERCCL;
+    // 3. merge + vote of the owned queries (ordered by distance, then global index)
+    if (m1 == m0) return hipStreamSynchronize(st) == hipSuccess ? KNN_OK : KNN_EHIP;
+    return knn_merge_vote_device(ctx, comm->nranks, m1 - m0, k, num_classes, (const int32_t*)comm->lists, d_pred,
+                                 d_dist, d_idx, st);
+}
+
+}  // extern "C"

@@ -46,8 +46,9 @@ def _c_strtol(s):
     return int(s[:j]) if j > i else 0
 
 
-def gpu_slice(train, test, k, start, end):
-    """The rank's KNN(train, test, k, start, end) (mpi.cpp:26) on its GPU."""
+def gpu_context():
+    """This rank's context on device LOCAL_RANK (mod the visible devices).  Created before
+    the timed region, as mpi.cpp:119-125's MPI_Init / rank setup is."""
     knn = _pkg()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     try:
@@ -55,15 +56,22 @@ def gpu_slice(train, test, k, start, end):
         ndev = max(1, torch.cuda.device_count())
     except ImportError:
         ndev = 1
-    ctx = knn.Context(local % ndev)
-    try:
+    return knn.Context(local % ndev, cache_train=True)
+
+
+def gpu_slice(ctx):
+    """The rank's KNN(train, test, k, start, end) (mpi.cpp:26) on its GPU context."""
+    knn = _pkg()
+
+    def compute(train, test, k, start, end):
         return knn.KNN_range(train, test, k, start, end, ctx=ctx)
-    finally:
-        ctx.close()
+    return compute
 
 
-def run(argv, compute=gpu_slice, out=sys.stdout):
-    """mpi.cpp main(); `compute` is the per-rank slice classifier (the GPU path)."""
+def run(argv, compute=None, out=sys.stdout):
+    """mpi.cpp main(); `compute` is the per-rank slice classifier (default: the GPU path on
+    a context made before the timed region).  With KNN_PRED_OUT set, rank 0 also writes the
+    gathered int32 predictions there (a test hook; the reference prints only its line)."""
     if len(argv) != 4:
         print(USAGE, file=out)
         return 0
@@ -77,6 +85,10 @@ def run(argv, compute=gpu_slice, out=sys.stdout):
         dist.init_process_group("gloo", rank=int(os.environ.get("RANK", "0")),
                                 world_size=int(os.environ.get("WORLD_SIZE", "1")))
     rank, world = dist.get_rank(), dist.get_world_size()
+    ctx = None
+    if compute is None:
+        ctx = gpu_context()
+        compute = gpu_slice(ctx)
     try:
         tf, tl, C = knn.read_arff(argv[1])
         qf, ql, Cq = knn.read_arff(argv[2])
@@ -103,9 +115,13 @@ def run(argv, compute=gpu_slice, out=sys.stdout):
             ms = (t1 - t0) // 1_000_000
             print(f"The {k}-NN classifier for {n} test instances on {len(tf)} train instances "
                   f"required {ms} ms CPU time. Accuracy was {acc:.4f}", file=out, flush=True)
+            if os.environ.get("KNN_PRED_OUT"):
+                np.asarray(full, np.int32).tofile(os.environ["KNN_PRED_OUT"])
             return full
         return None
     finally:
+        if ctx is not None:
+            ctx.close()
         if own_group:
             dist.destroy_process_group()
 

@@ -27,6 +27,13 @@ def test_library_exports_every_header_symbol(knn):
     assert lib.knn_version() == 2
 
 
+def test_library_built_from_this_tree(knn):
+    """knn_build_id() (baked in by the Makefile) equals the hash of the sources beside the
+    library: the .so the tests load is the one these sources build."""
+    built, tree = knn.build_id()
+    assert built == tree
+
+
 def test_cpp_surface_symbols_exported():
     out = subprocess.run(["nm", "-DC", "--defined-only", os.path.join(PKG_DIR, "libknn_amd.so")],
                          capture_output=True, text=True, check=True).stdout
@@ -148,6 +155,27 @@ def test_shard_range_rule(knn):
             rs = [knn.shard_range(n, w, r) for r in range(w)]
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
+
+
+def test_c_shard_range_and_exchange_layout(knn):
+    """knn_shard_range / knn_exchange_layout (the C ABI's train-sharded exchange plan,
+    knn_comm.cpp) agree with shard_range and exchange_shard_lists' all-to-all split."""
+    for n in (0, 1, 7, 100, 1718, 1_000_003):
+        for w in (1, 2, 3, 8):
+            for r in range(w):
+                assert knn.shard_range_c(n, w, r) == knn.shard_range(n, w, r)
+    for nq, k, w in ((100, 10, 1), (1000, 7, 3), (5, 3, 8), (1_000_000, 100, 8)):
+        spans = [knn.shard_range(nq, w, r) for r in range(w)]
+        for r in range(w):
+            so, sc, ro, rc = knn.exchange_layout(nq, k, w, r)
+            mine = (spans[r][1] - spans[r][0]) * 3 * k
+            assert list(sc) == [(b - a) * 3 * k for a, b in spans]
+            assert list(so) == list(np.concatenate([[0], np.cumsum(sc)[:-1]]))
+            assert list(rc) == [mine] * w and list(ro) == [b * mine for b in range(w)]
+    with pytest.raises(knn.KnnError):
+        knn.exchange_layout(10, 0, 2, 0)
+    with pytest.raises(knn.KnnError):
+        knn.shard_range_c(10, 2, 2)
 
 
 # --- multi-threaded ingestion (SURVEY.md 8f row 1) ------------------------------------

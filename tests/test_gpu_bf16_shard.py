@@ -172,3 +172,43 @@ def test_config_c_shard_sampled(knn, oracle):
     assert np.array_equal(dd[qs].view(np.uint32), odist.view(np.uint32))
     assert np.array_equal(r[qs, 2, :], lab[oidx])
     c.close()
+
+
+@pytest.mark.parametrize("dtype,d,k,nt,nq", [("f32", 128, 10, 20000, 257), ("bf16", 256, 100, 24000, 100)])
+def test_rccl_train_sharded_single_rank(knn, oracle, dtype, d, k, nt, nq):
+    """knn_predict_train_sharded behind the C ABI with a one-rank RCCL communicator
+    (knn_comm_create, dlopen'd RCCL): shard top-k -> grouped ncclSend/ncclRecv -> merge +
+    vote.  Two calls on two halves of the train set with idx_base show the global-index
+    bookkeeping; the full set must equal the oracle bit for bit (main.cpp:40-82)."""
+    import torch
+    kind = 1 if dtype == "bf16" else 0
+    trf, tl = oracle.gen(13, 0, 0, nt, d, kind=kind)
+    tef, _ = oracle.gen(13, 1, 0, nq, d, kind=kind)
+    bad, opred, odist, oidx = oracle.knn(trf, tl, tef, k, 10)
+    assert bad == 0
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    train = torch.from_numpy(trf).to("cuda:0").to(tdt)
+    test = torch.from_numpy(tef).to("cuda:0").to(tdt)
+    labels = torch.from_numpy(tl).to("cuda:0")
+    ctx = knn.Context(0)
+    comm = knn.Comm(ctx, knn.comm_unique_id(), 1, 0)
+    try:
+        pred = torch.empty(nq, dtype=torch.int32, device="cuda:0")
+        dist = torch.empty((nq, k), dtype=torch.float32, device="cuda:0")
+        idx = torch.empty((nq, k), dtype=torch.int32, device="cuda:0")
+        q0, q1 = comm.predict_train_sharded(train, labels, 0, test, k, 10, pred, dist, idx)
+        torch.cuda.synchronize()
+        assert (q0, q1) == (0, nq)
+        assert np.array_equal(idx.cpu().numpy(), oidx)
+        assert np.array_equal(dist.cpu().numpy().view(np.uint32), odist.view(np.uint32))
+        assert np.array_equal(pred.cpu().numpy(), opred)
+        # the second half alone, placed at its global offset
+        h = nt // 2
+        bad, hp, hd, hi = oracle.knn(trf[h:], tl[h:], tef, k, 10)
+        comm.predict_train_sharded(train[h:], labels[h:], h, test, k, 10, pred, dist, idx)
+        torch.cuda.synchronize()
+        assert np.array_equal(idx.cpu().numpy(), hi + h)
+        assert np.array_equal(pred.cpu().numpy(), hp)
+    finally:
+        comm.close()
+        ctx.close()

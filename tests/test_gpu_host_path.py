@@ -119,3 +119,10 @@ def test_pinned_buffers(knn, oracle):
         ctx.close()
         ptr.free()
         pte.free()
+
+
+def test_loaded_library_is_this_trees(knn):
+    """The libknn_amd.so these GPU tests load was built from the sources beside it
+    (knn_build_id() == build_id.py's hash of the tree)."""
+    built, tree = knn.build_id()
+    assert built == tree

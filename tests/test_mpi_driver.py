@@ -85,8 +85,9 @@ def test_mpi_strtol():
 
 
 @pytest.mark.gpu
-def test_mpi_driver_torchrun_two_ranks_one_gpu():
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+def test_mpi_driver_torchrun_two_ranks_one_gpu(tmp_path):
+    out = tmp_path / "pred.bin"
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", KNN_PRED_OUT=str(out))
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                         "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
                         os.path.join(PKG_DIR, "mpi_driver.py"), f"{DATA}/large-train.arff",
@@ -97,3 +98,5 @@ def test_mpi_driver_torchrun_two_ranks_one_gpu():
     assert len(lines) == 1, r.stdout
     m = LINE.match(lines[0])
     assert m and m.group(5) == "0.9948" and m.group(2) == "1718" and m.group(3) == "30803"
+    # the gathered predictions are the reference's, byte for byte
+    assert pred_sha(np.fromfile(out, np.int32)) == golden_manifest()["large_k5"]["sha256"]

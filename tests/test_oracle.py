@@ -3,10 +3,13 @@
 The fixtures in tests/golden/ were captured from the reference itself
 (oracle/ref_capture.cpp around /root/reference/main.cpp; tests/golden/make_golden.py).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
-from conftest import (DATA, DATASETS, KS, golden_cm, golden_manifest, golden_pred, golden_topk,
+from conftest import (ORACLE_DIR, DATA, DATASETS, KS, golden_cm, golden_manifest, golden_pred, golden_topk,
                       pred_sha)
 
 SURVEY_SHA = {  # SURVEY.md 8c, captured independently by the survey
@@ -98,3 +101,44 @@ def test_oracle_k_above_n_flags(oracle):
     tr = np.zeros((3, 2), np.float32)
     bad, *_ = oracle.knn(tr, np.zeros(3, np.int32), tr, 4, 1)
     assert bad == 1
+
+
+# --- the reference's MPI path (cpu_baseline "mpi" leg) ----------------------------------
+def _ref_mpi(name):
+    p = os.path.join(ORACLE_DIR, "_ref", name)
+    if not (os.path.exists(p) and os.path.exists("/opt/conda/bin/mpiexec")):
+        pytest.skip("reference MPI build absent")
+    return p
+
+
+def test_reference_mpi_bench_matches_pthreads_and_oracle(oracle, tmp_path):
+    """ref_bench_mpi (mpi.cpp's KNN + Scatter/Gatherv under mpiexec) and ref_bench
+    (multi-thread.cpp's KNN) give the oracle's predictions on the same generated sample."""
+    import subprocess
+    argv = ["0", "7", "3000", "61", "32", "5", "10"]
+    r = subprocess.run(["/opt/conda/bin/mpiexec", "-n", "3", _ref_mpi("ref_bench_mpi")] + argv +
+                       [str(tmp_path / "mpi.txt")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["ranks"] == 3 and rec["nq"] == 61
+    r = subprocess.run([_ref_mpi("ref_bench")] + argv + ["2", str(tmp_path / "mt.txt")], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    mpi = np.loadtxt(tmp_path / "mpi.txt", dtype=np.int32)
+    mt = np.loadtxt(tmp_path / "mt.txt", dtype=np.int32)
+    tr, tl = oracle.gen(7, 0, 0, 3000, 32)
+    te, _ = oracle.gen(7, 1, 0, 61, 32)
+    _, opred, _, _ = oracle.knn(tr, tl, te, 5, 10)
+    assert np.array_equal(mpi, opred) and np.array_equal(mt, opred)
+
+
+def test_reference_mpi_binary_line():
+    """The reference's own mpi binary (mpi.cpp built with MPICH) on the small pair: its
+    line carries the golden accuracy (the line the drop-in driver must reproduce)."""
+    import re
+    import subprocess
+    r = subprocess.run(["/opt/conda/bin/mpiexec", "-n", "2", _ref_mpi("mpi"), f"{DATA}/small-train.arff",
+                        f"{DATA}/small-test.arff", "3"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    m = re.search(r"Accuracy was (\d\.\d{4})", r.stdout)
+    assert m and m.group(1) == f"{golden_manifest()['small_k3']['accuracy']:.4f}"
