@@ -180,10 +180,15 @@ def bench_arff(args, knn, torch, local):
     elapsed = time.perf_counter() - t0
     got = pred.cpu().numpy()
     want = np.loadtxt(os.path.join(REPO, ARFF_L[2]), dtype=np.int32)
-    # host buffers in, predictions out (knn_predict: uploads inside the call, PCIe-inclusive)
-    t1 = time.perf_counter()
-    host_pred = ctx.predict(tf, tl, qf, k, C)
-    host_ms = 1e3 * (time.perf_counter() - t1)
+    # host buffers in, predictions out (knn_predict: uploads inside the call, PCIe-inclusive):
+    # cold = first call on a caching context (train uploaded), warm = the next one
+    hctx = knn.Context(local, algo=args.algo, cache_train=True)
+    host_ms = {}
+    for phase in ("cold", "warm"):
+        t1 = time.perf_counter()
+        host_pred = hctx.predict(tf, tl, qf, k, C)
+        host_ms[phase] = round(1e3 * (time.perf_counter() - t1), 3)
+    hctx.close()
     cm = knn.computeConfusionMatrix(got, ql, C)
     pairs = float(nt) * nq * args.steps
     stages = {n: v / args.steps for n, v in stage_sum.items()}
@@ -208,12 +213,54 @@ def bench_arff(args, knn, torch, local):
         "bit_match": {"predictions_equal_reference": bool(np.array_equal(got, want)),
                       "host_path_equal": bool(np.array_equal(host_pred, want)),
                       "accuracy": float(np.float32(np.trace(cm)) / np.float32(nq))},
-        "host_buffers_ms": round(host_ms, 3),
+        "host_buffers_ms": host_ms,
         "roofline": roof,
         "cpu_baseline": None if args.no_cpu_baseline else cpu_baseline_arff(k),
     }
     print(json.dumps(out), flush=True)
     ctx.close()
+
+
+def host_buffer_times(knn, local, algo, train, labels, test, k, C, pred_dev):
+    """PCIe-inclusive rates (never `value`): the same KNN call from host buffers through
+    knn_predict (main.cpp:25's KNN on host data).  cold = first call on a context with the
+    train cache (train + queries uploaded), warm = the next call (train cached, queries
+    streamed in batches through two slots overlapping compute), for pageable numpy arrays
+    and for page-locked buffers (knn_alloc_pinned).  Predictions must equal the resident
+    run's."""
+    import torch
+    tr, tl, te = train.cpu().numpy(), labels.cpu().numpy(), test.cpu().numpy()
+    want = pred_dev.cpu().numpy()
+    out = {"note": "knn_predict on host buffers, PCIe-inclusive (H2D of train when cold, of the "
+                   "queries always, D2H of predictions); the headline value keeps inputs in HBM"}
+    nt, nq = tr.shape[0], te.shape[0]
+    pinned = []
+    for kind in ("pageable", "pinned"):
+        if kind == "pinned":
+            ptr, pte = knn.PinnedArray(tr.shape, np.float32), knn.PinnedArray(te.shape, np.float32)
+            ptr.array[:] = tr
+            pte.array[:] = te
+            pinned = [ptr, pte]
+            a_tr, a_te = ptr.array, pte.array
+        else:
+            a_tr, a_te = tr, te
+        ctx = knn.Context(local, algo=algo, cache_train=True)
+        rec = {}
+        for phase in ("cold", "warm"):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            got = ctx.predict(a_tr, tl, a_te, k, C)
+            ms = 1e3 * (time.perf_counter() - t0)
+            st = ctx.stats()
+            rec[phase + "_ms"] = round(ms, 2)
+            rec[phase + "_pairs_per_s"] = nt * nq / (ms * 1e-3)
+            rec[phase + "_h2d_bytes"] = st["h2d_train_bytes"] + st["h2d_query_bytes"]
+            rec[phase + "_equal_resident"] = bool(np.array_equal(got, want))
+        ctx.close()
+        out[kind] = rec
+    for p in pinned:
+        p.free()
+    return out
 
 
 def pmc_traffic(config):
@@ -234,6 +281,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="A", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exchange", default="rccl", choices=["rccl", "torch"],
+                    help="train-sharded configs: C-ABI RCCL communicator or torch.distributed all-to-all")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-buffer calls")
     ap.add_argument("--algo", default="auto", choices=["auto", "gemm", "gemm_split", "gemm_bf16", "direct"])
     ap.add_argument("--splits", type=int, default=0, help="train segments per query tile (0 = auto)")
     ap.add_argument("--nt", type=int, default=0, help="override train rows (kernel studies)")
@@ -294,12 +344,30 @@ def main():
         own0, own1 = knn.shard_range(nq, world, rank)
         pred = torch.empty(own1 - own0, dtype=torch.int32, device=dev)
     cur = torch.cuda.current_stream(dev).cuda_stream
+    # train-sharded exchange: the C ABI's RCCL communicator (knn_predict_train_sharded) by
+    # default; "torch" = exchange_shard_lists over torch.distributed (the only choice when
+    # ranks share a GPU: RCCL wants one rank per device)
+    exchange = args.exchange if not share else "torch"
+    comm = None
+    if sharding == "train" and exchange == "rccl":
+        uid = [knn.comm_unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        comm = knn.Comm(ctx, uid[0], world, rank)
 
     def step():
         if sharding == "test":
             ctx.predict_device(train, labels, test, k, C, pred)
             return ctx.stage_times()
-        # per-shard exact top-k -> all-to-all (RCCL) -> merge + vote, on one stream
+        if comm is not None:
+            # shard top-k -> grouped ncclSend/Recv -> merge + vote, one stream, one C call
+            t_x = time.perf_counter()
+            comm.predict_train_sharded(train, labels, t0_row, test, k, C, pred, stream=cur)
+            torch.cuda.current_stream(dev).synchronize()
+            times = ctx.stage_times()
+            times["train_sharded_wall"] = 1e3 * (time.perf_counter() - t_x)
+            return times
+        # per-shard exact top-k -> all-to-all (torch.distributed) -> merge + vote, on one stream
         ctx.shard_topk_device(train, labels, test, k, C, t0_row, rec, stream=cur)
         times = ctx.stage_times()
         t_x = time.perf_counter()
@@ -335,9 +403,11 @@ def main():
     # select stage (k_rescore): one untimed diagnostic pass counts the filter's candidates,
     # giving the rescore's algorithmic bytes (select stage vs HBM)
     select = None
-    if rank == 0 and "rescore" in stage_sum:
+    if "rescore" in stage_sum:  # every rank: a train-sharded step is collective
         ctx.close()
         ctx = knn.Context(local, algo=args.algo, train_splits=args.splits, profile=2)
+        if comm is not None:
+            comm.ctx = ctx  # the communicator is bound to a device, the context per call
         step()
         cand = ctx.stats()["candidates"]
         stats["candidates"] = cand  # the timed steps do not count them (profile=2 pass only)
@@ -351,6 +421,9 @@ def main():
                   "candidates_per_query": round(cand / nq, 1), "algorithmic_bytes": byts,
                   "achieved": round(byts / (resc_ms * 1e-3) / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
                   "frac": round(byts / (resc_ms * 1e-3) / 1e9 / 8000.0, 4)}
+    host = None
+    if rank == 0 and world == 1 and sharding == "test" and not args.no_host_path:
+        host = host_buffer_times(knn, local, args.algo, train, labels, test, k, C, pred)
     total_q = nq_cfg * world if scaling == "weak" else nq_cfg
     gathered = None
     if world > 1:  # outside the timed region: rank 0 collects predictions (mpi.cpp:186)
@@ -388,7 +461,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(d, k, C, seed, kind)
         par = (f"test-sharded dp{world}, train replicated" if sharding == "test" else
-               f"train-sharded x{world} (shard_range of train rows), all-to-all of per-shard top-k, merge")
+               f"train-sharded x{world} (shard_range of train rows), all-to-all of per-shard top-k "
+               f"({'RCCL via knn_predict_train_sharded' if comm is not None else 'torch.distributed'}), merge")
         out = {
             "metric": METRIC, "value": pairs / elapsed, "unit": "pairs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
@@ -405,8 +479,11 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "select_stage": select,
+            "host_buffers": host,
         }
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

@@ -64,7 +64,8 @@ struct knn_ctx {
     DBuf tmax;              // fused filter: per-64-row maximum train norm
     // kernel-study switches, read once from the environment in knn_create (never in a call)
     int study_seed = 0, study_timing = 0, study_nofused = 0;
-    FilterStudy fstudy{0, {0}, -1};
+    int rescore_su = 0;  // test hook KNN_RESCORE_SU: the rescore's LDS staging size (0 = sized)
+    FilterStudy fstudy{0, {0}, -1, -1};
     // host-API staging (device copies of host inputs / outputs)
     DBuf h_train, h_labels, h_test, h_pred, h_dist, h_idx;
     int32_t* ctrl_host = nullptr;  // pinned: [0] status, [1] fallback count
@@ -499,6 +500,14 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     r.out = out; r.status = c->ctrl.as<int32_t>();
     r.fb_list = c->fb_list.as<int32_t>(); r.fb_count = c->ctrl.as<int32_t>() + 1;
     r.gate = gate;
+    // LDS staging for about twice the expected kept rows -- k (1 + ln(nt / k)) for one scan,
+    // +25 % per extra segment (they share thresholds through gthr), measured 238 per query on
+    // A and 605 on B -- rounded to 64 by the launcher and capped at the list capacity: a
+    // smaller footprint per wave lets more query waves share a CU
+    {
+        const double expect = k * (1.0 + std::log(std::max((double)nt / k, 1.0))) * (1.0 + 0.25 * (nseg - 1)) + 64.0;
+        r.su_cap = c->rescore_su > 0 ? c->rescore_su : (int)std::min<double>(cap, 2.0 * expect);
+    }
     stage_begin(c, st, gate ? "rescore_rerun" : "rescore");
     HIP_OR_FAIL(c, knn_launch_rescore(r, st));
     stage_end(c, st);
@@ -541,6 +550,8 @@ knn_status knn_create(knn_ctx** out, const knn_opts* opts) {
     if (const char* e = getenv("KNN_FILTER_FUSED")) c->study_nofused = atoi(e) == 0;
     if (const char* e = getenv("KNN_FILTER_NBUF")) c->fstudy.nbuf = atoi(e);
     if (const char* e = getenv("KNN_FILTER_PSTEP")) c->fstudy.pstep = atoi(e);
+    if (const char* e = getenv("KNN_FILTER_KR")) c->fstudy.kr = atoi(e);
+    if (const char* e = getenv("KNN_RESCORE_SU")) c->rescore_su = atoi(e);
     if (const char* e = getenv("KNN_FILTER_SHAPE")) snprintf(c->fstudy.shape, sizeof(c->fstudy.shape), "%s", e);
     if (c->device < 0 || c->device >= ndev) { delete c; return KNN_ENODEV; }
     hipDeviceProp_t prop;

@@ -34,6 +34,7 @@
 #define KNN_FUSED_RQ 4  // deferred-queue depth per lane
 #endif
 
+
 // ---------------------------------------------------------------------------------
 // k_aug_rows<E>: rows of the fused filter, [n][d + 16] bf16.  Element c < d is
 // rn(scale * x[r][c]) (scale = 1: train, -2: queries; exact scaling by a power of two);
@@ -110,7 +111,7 @@ hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int ld, int d
 // max-heap in LDS, as k_gemm_filter), or a smaller bound published by another segment
 // (gthr).  Every row of the exact top-k has L <= D <= D_(k) <= thr, so it is kept.
 // ---------------------------------------------------------------------------------
-template <int RB, int MINW, int NBUF, int NW, int RG, bool PSTEP>
+template <int RB, int MINW, int NBUF, int NW, int RG, bool PSTEP, int KR>
 __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) {
     if ((a.gate && *a.gate == 0) || (*a.status & KNN_STATUS_GEMM_UNSAFE)) return;  // not taken / exact path
     typedef FilterTile<RB, NW, 1, RG> FT;
@@ -124,6 +125,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
     constexpr int RS = BN;                       // ring slot: BN row norms
     static_assert(NBUF == 2 || NBUF == 3, "tile buffers");
     static_assert(RG == 1 || RG == 2, "row groups");
+    static_assert(KR == 0 || KR == 16, "register list length");
+    constexpr bool RL = KR > 0;  // thresholds from per-lane register lists (else LDS heaps)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* tiles = smem;                                     // [NBUF][TILE]
     float* ring = reinterpret_cast<float*>(smem + NBUF * TILE);      // [NR][RS] train norms tn
@@ -145,9 +148,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
     const int64_t ldb = (int64_t)a.ld_t * 2;  // augmented train row pitch, bytes
     const unsigned char* trainb = reinterpret_cast<const unsigned char*>(a.train);
 
-    for (int i = threadIdx.x; i < BM * hs; i += NT) {
-        const int e = i % hs;
-        topU[i] = (e == hs - 1 || e <= k - 2) ? INF : -INF;  // root, nodes 1..k-1: +inf
+    if constexpr (!RL) {
+        for (int i = threadIdx.x; i < BM * hs; i += NT) {
+            const int e = i % hs;
+            topU[i] = (e == hs - 1 || e <= k - 2) ? INF : -INF;  // root, nodes 1..k-1: +inf
+        }
     }
     for (int i = threadIdx.x; i < NR * RS; i += NT) ring[i] = INF;
 
@@ -174,6 +179,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
     };
     make_tfb();
     auto tf_of = [&](float tm) __attribute__((always_inline)) { return fmaf(coef + 0x1p-18f, tm, tfb); };
+
+    const int ntiles = (row_end > row_begin) ? (int)((row_end - row_begin + BN - 1) / BN) : 0;
 
     // ---- LDS-DMA of tiles (same image as k_gemm_filter: slot P -> row P / SLOTS, slot P % SLOTS,
     // the pad slot duplicates slot 0; rows past nt read row nt-1 and are rejected by index)
@@ -290,13 +297,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
 #define KNN_TSTAMP(v)
 #endif
 
-    // keep candidate (L, U) of global row t: the exact test against the current threshold,
-    // the candidate store into this lane half's sub-slice, and, if U beats the heap root, a
-    // sift-down of the query's 4-ary max-heap (node n >= 1 in H[n-1], the root in H[hs-1]:
-    // the four children of node i are one aligned 16-byte read at H[4i]).  Only one lane of
-    // a query runs it at a time.
-    auto accept = [&](float L, float U, int64_t t) __attribute__((always_inline)) {
-        if (!(L <= thr)) return;
+    // append candidate (L, U) of global row t to this lane half's sub-slice (past its
+    // capacity: counted only, the rescore then sends the query to the exact scan)
+    auto store_cand = [&](float L, float U, int64_t t) __attribute__((always_inline)) {
         if (ccnt < cap_sub) {
             const int64_t o = q * (int64_t)a.cap + (int64_t)(2 * seg + h) * cap_sub + ccnt;
             a.cand_idx[o] = (int32_t)t;
@@ -304,6 +307,15 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
             a.cand_U[o] = U;
         }
         ccnt++;
+    };
+    // keep candidate (L, U) of global row t: the exact test against the current threshold,
+    // the candidate store into this lane half's sub-slice, and, if U beats the heap root, a
+    // sift-down of the query's 4-ary max-heap (node n >= 1 in H[n-1], the root in H[hs-1]:
+    // the four children of node i are one aligned 16-byte read at H[4i]).  Only one lane of
+    // a query runs it at a time.
+    auto accept = [&](float L, float U, int64_t t) __attribute__((always_inline)) {
+        if (!(L <= thr)) return;
+        store_cand(L, U, t);
         if (U < root) {
             float* H = topU + jl * hs;
             int i = 0;
@@ -355,8 +367,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
         if constexpr (NACC == 1) return Y[0][v & 15];
         else return (v >> 4) ? Y[1][v & 15] : Y[0][v & 15];
     };
-    // the values of Y some lane passes (bit 16c + r), for the !PSTEP variant: one v_cmp per
-    // value into an SGPR pair, then scalar ops (only on tiles some value passes)
+    // the values of Y some lane passes (bit 16c + r): one v_cmp per value into an SGPR pair,
+    // then scalar ops (the !PSTEP variant builds it only on tiles some value passes).
+    // Measured (same box): sets by groups of 4 values (a min of 4 per ballot) are slower on A
+    // and B -- the extra slow-path visits cost more than the scalar ops they save.
     auto pass_set = [&](floatx16 (&Y)[NACC], float tf) __attribute__((always_inline)) -> uint32_t {
         uint32_t u = 0u;
 #pragma unroll
@@ -390,6 +404,53 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
             }
         }
         publish();
+    };
+
+    // register-list slow path (KR > 0): both lanes of a query (its two row halves) keep the
+    // same ascending list lst[] of the KR smallest U of the query's kept candidates -- the
+    // first KR - k entries are -inf pads, so lst[KR-1] is the k-th smallest real U, an upper
+    // bound on D_(k) (k rows with D <= U <= it).  Per passing value the two lanes swap their
+    // candidate U (v_permlane32_swap) and both insert both (2 KR v_med3, the multiset and so
+    // the list come out the same in either order): the query's exact k-th smallest, like the
+    // heap, for all 32 queries of the wave at once -- no LDS, no lane takes turns.
+    float lst[RL ? KR : 1];
+    if constexpr (RL) {
+#pragma unroll
+        for (int i = 0; i < KR; i++) lst[i] = i < KR - k ? -INF : INF;
+    }
+    auto list_insert = [&](float w) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = KR - 1; i >= 1; i--) lst[i] = __builtin_amdgcn_fmed3f(lst[i - 1], w, lst[i]);
+        lst[0] = fminf(lst[0], w);
+    };
+    auto slow_rl = [&](floatx16 (&Y)[NACC], int tp, float tf, uint32_t u) {
+        if constexpr (RL) {
+            const int64_t tbase = row_begin + (int64_t)tp * BN;
+            if constexpr (!PSTEP) u = pass_set(Y, tf);
+            while (u) {
+                const int v = __builtin_ctz(u);
+                u &= u - 1u;
+                const float y = yval(Y, v);
+                const int r = v & 15;
+                const int row = 32 * (v >> 4) + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int64_t t = tbase + row;
+                float L, U;
+                bounds(y, row, tp, L, U);
+                const bool keep = y <= tf && t < row_end && L <= thr;
+                if (keep) store_cand(L, U, t);
+                const float w = (keep && U < lst[KR - 1]) ? U : INF;
+                // one result of the swap is this lane's own word, the other its partner's
+                const uint32_t wb = __float_as_uint(w);
+                const auto sw = __builtin_amdgcn_permlane32_swap(wb, wb, false, false);
+                const float wp = __uint_as_float(sw[0] == wb ? sw[1] : sw[0]);  // the other half's
+                if (__ballot(w < INF || wp < INF)) {
+                    list_insert(w);
+                    list_insert(wp);
+                    thr = fminf(thr, lst[KR - 1]);
+                }
+            }
+            make_tfb();
+        }
     };
 
     // deferred slow path (8-wave shapes): passing values with L <= thr are queued -- (L, U,
@@ -459,7 +520,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
         }
     };
 
-    const int ntiles = (row_end > row_begin) ? (int)((row_end - row_begin + BN - 1) / BN) : 0;
     floatx16 accA[NACC], accB[NACC];
 #pragma unroll
     for (int c = 0; c < NACC; c++) accA[c] = accB[c] = floatx16{};
@@ -471,17 +531,24 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
 #define KNN_FUSED_EARLY_DMA 0
 #endif
     constexpr bool LATE_DMA = NBUF == 3 && !KNN_FUSED_EARLY_DMA;
-    constexpr bool DEFER = NW == 8 && KNN_FUSED_DEFER;
+    constexpr bool DEFER = NW == 8 && KNN_FUSED_DEFER && !RL;
     constexpr int DEFER_EVERY = KNN_FUSED_DEFER_EVERY;
     // per-64-row maximum train norm of the tile in the pipeline (tile it) and of tile it-1
     const float* tmaxp = a.tmax + (row_begin >> 6);
     float tm_prev = 0.0f;
     auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
-        const int64_t r0 = row_begin + (int64_t)it * BN;
-        if ((it & 63) == 63 && a.nseg > 1 && qvalid) {
-            // thresholds published by other segments of this query
-            const float gv = o2f(__hip_atomic_load(&a.gthr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            if (gv < thr) { thr = gv; make_tfb(); }
+        if ((it & 63) == 63) {
+            if (a.nseg > 1 && qvalid) {
+                if constexpr (RL) {  // publish this query's bound (the heap path does it per accept)
+                    if (h == 0 && thr < published) {
+                        atomicMin(&a.gthr[q], f2o(thr));
+                        published = thr;
+                    }
+                }
+                // thresholds published by other segments of this query
+                const float gv = o2f(__hip_atomic_load(&a.gthr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if (gv < thr) { thr = gv; make_tfb(); }
+            }
         }
         const bool keep_next = NBUF == 3 && it + 1 < ntiles && (LATE_DMA || !dirty);
         KNN_TSTAMP(t0);
@@ -496,13 +563,14 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
 #else
         const bool dma_on = false;
 #endif
-        const DmaTile dd = dma_desc((it + NBUF - 1) % NBUF, (it + NBUF - 1) % NR, r0 + (int64_t)(NBUF - 1) * BN);
+        const DmaTile dd = dma_desc((it + NBUF - 1) % NBUF, (it + NBUF - 1) % NR, row_begin + (int64_t)(it + NBUF - 1) * BN);
         const float tf = it > 0 ? tf_of(tm_prev) : -INF;
         const uint32_t uY = step(X, Y, it % NBUF, dma_on && !LATE_DMA, dd, tf);
         KNN_TSTAMP(t2);
 #ifndef KNN_ABLATE_NO_SLOW
         if (uY) {
-            if constexpr (DEFER) record(Y, it - 1, tf, uY);
+            if constexpr (RL) { slow_rl(Y, it - 1, tf, uY); dirty = true; }
+            else if constexpr (DEFER) record(Y, it - 1, tf, uY);
             else { slow(Y, it - 1, tf, uY); dirty = true; }
         }
         if constexpr (DEFER) {
@@ -533,13 +601,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
         const int last = ntiles - 1;
         auto drain = [&](floatx16 (&Lc)[NACC]) {
             const float tf = tf_of(tm_prev);
-            uint32_t u = 0u;
-#pragma unroll
-            for (int c = 0; c < NACC; c++)
-#pragma unroll
-                for (int r = 0; r < 16; r++) u |= (__ballot(Lc[c][r] <= tf) != 0ull ? 1u : 0u) << (16 * c + r);
+            const uint32_t u = pass_set(Lc, tf);
             if (u) {
-                if constexpr (DEFER) record(Lc, last, tf, u);
+                if constexpr (RL) slow_rl(Lc, last, tf, u);
+                else if constexpr (DEFER) record(Lc, last, tf, u);
                 else slow(Lc, last, tf, u);
             }
         };
@@ -548,6 +613,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
     }
     if constexpr (DEFER) {
         if (__ballot(qcnt > 0)) flush();
+    }
+    if constexpr (RL) {  // the final bound of this segment, for the other segments' rescore
+        if (a.nseg > 1 && qvalid && h == 0 && thr < published) atomicMin(&a.gthr[q], f2o(thr));
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -570,10 +638,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
 // ---------------------------------------------------------------------------------
 // plan and launch
 // ---------------------------------------------------------------------------------
-static size_t fused_lds_of(int row_bytes, int k, int nw, int rg, int nbuf) {
+static size_t fused_lds_of(int row_bytes, int k, int nw, int rg, int nbuf, bool heaps) {
     const int bn = 32 * rg, bm = 32 * nw;
     const int ins = (bn * (row_bytes / 16 + 1) + 63) / 64;
-    return (size_t)nbuf * ins * 1024 + ((size_t)(nbuf + 1) * bn + (size_t)bm * heap_stride(k)) * sizeof(float);
+    return (size_t)nbuf * ins * 1024 + ((size_t)(nbuf + 1) * bn + (heaps ? (size_t)bm * heap_stride(k) : 0)) * sizeof(float);
 }
 
 bool knn_fused_supported(int d) { return d == 64 || d == 128 || d == 256; }
@@ -583,20 +651,26 @@ bool knn_fused_supported(int d) { return d == 64 || d == 128 || d == 256; }
 //            barrier and fast test outweigh 5 MFMAs per 32x32 block; the other block hides them)
 //  d >= 128: 8 waves x 32 queries (two waves per SIMD), 64-row tiles, double-buffered; 32-row
 //            tiles when the per-query heaps of a large k leave no room for 64-row tiles.
+// Thresholds: k <= 16 keeps per-query register lists (KR = 16), larger k the LDS heaps
+// (measured on B, k = 32: 32-entry lists cost a block per CU of occupancy and 9 % of time).
 FilterPlan knn_fused_plan(int d, int k, const FilterStudy* fs) {
     const int rb = 2 * d + 32;
-    const size_t cap = 160 * 1024;
+    const size_t cap = 160 * 1024 - 256;  // room for the kernel's static LDS (the start tile)
     // pass-set variant (FilterPlan.qg): in-step for d >= 128; KNN_FILTER_PSTEP overrides (study)
     const int pstep = fs && fs->pstep >= 0 ? fs->pstep : (d >= 128 ? 1 : 0);
+    int kr = k <= 16 ? 16 : 0;
+    if (fs && fs->kr == 0) kr = 0;  // study: the heaps for every k
     auto make = [&](int nw, int rg, int minw, int nbuf) {
-        return FilterPlan{nw, pstep, rg, minw, nbuf, 32 * nw, fused_lds_of(rb, k, nw, rg, nbuf)};
+        FilterPlan f{nw, pstep, rg, minw, nbuf, 32 * nw, fused_lds_of(rb, k, nw, rg, nbuf, kr == 0)};
+        f.kr = kr;
+        return f;
     };
     const bool force8 = fs && fs->shape[0] == 'w' && fs->shape[1] == '8';
     const int nb = fs && fs->nbuf == 3 ? 3 : 2;  // kernel study: triple-buffered tiles
     const bool force4 = fs && fs->shape[0] == 'w' && fs->shape[1] == '4';
-    if ((d == 64 || force4) && !force8 && fused_lds_of(rb, k, 4, 2, nb) <= cap / 2) return make(4, 2, 2, nb);
-    if (fused_lds_of(rb, k, 8, 2, nb) <= cap) return make(8, 2, 2, nb);
-    if (fused_lds_of(rb, k, 8, 1, 2) <= cap) return make(8, 1, 2, 2);
+    if ((d == 64 || force4) && !force8 && fused_lds_of(rb, k, 4, 2, nb, kr == 0) <= cap / 2) return make(4, 2, 2, nb);
+    if (fused_lds_of(rb, k, 8, 2, nb, kr == 0) <= cap) return make(8, 2, 2, nb);
+    if (fused_lds_of(rb, k, 8, 1, 2, kr == 0) <= cap) return make(8, 1, 2, 2);
     return FilterPlan{0, 0, 0, 0, 0, 0, 0};  // k too large for the LDS heaps: not supported
 }
 
@@ -604,17 +678,21 @@ FilterPlan knn_fused_plan(int d, int k, const FilterStudy* fs) {
 // (PSTEP: a v_cmp per value between the MFMAs; d >= 128, where the MFMAs hide it), 0 = a
 // v_min3 chain in the step and the set built on passing tiles only (d = 64: 10 MFMAs per
 // tile leave no room).  Measured on one box: A (d = 128) PSTEP faster, B (d = 64) slower.
-template <int RB, bool P>
+template <int RB, bool P, int KR>
 static const void* fused_fn_p(const FilterPlan& f) {
-#define KNN_FUSED_FN(NB, NW, RG) reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, NB, NW, RG, P>)
+#define KNN_FUSED_FN(NB, NW, RG) reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, NB, NW, RG, P, KR>)
     if (f.nw == 4) return f.nbuf == 3 ? KNN_FUSED_FN(3, 4, 2) : KNN_FUSED_FN(2, 4, 2);
     if (f.rg == 2) return f.nbuf == 3 ? KNN_FUSED_FN(3, 8, 2) : KNN_FUSED_FN(2, 8, 2);
     return KNN_FUSED_FN(2, 8, 1);
 #undef KNN_FUSED_FN
 }
+template <int RB, bool P>
+static const void* fused_fn_k(const FilterPlan& f) {
+    return f.kr == 16 ? fused_fn_p<RB, P, 16>(f) : fused_fn_p<RB, P, 0>(f);
+}
 template <int RB>
 static const void* fused_fn(const FilterPlan& f) {
-    return f.qg ? fused_fn_p<RB, true>(f) : fused_fn_p<RB, false>(f);
+    return f.qg ? fused_fn_k<RB, true>(f) : fused_fn_k<RB, false>(f);
 }
 
 static const void* fused_ptr(int d, const FilterPlan& f) {

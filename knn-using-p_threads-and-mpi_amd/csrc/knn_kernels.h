@@ -62,6 +62,7 @@ struct RescoreArgs {
     QueryOut out; int32_t* status;
     int32_t* fb_list; int32_t* fb_count;
     const int32_t* gate;  // optional: runs only when *gate != 0 (AUTO's re-run)
+    int su_cap;           // candidates staged in LDS per query (host: ~3x the expected count)
     int q_lds_bytes; int c_lds_bytes; int wave_lds_bytes;  // set by the launcher
 };
 
@@ -123,10 +124,13 @@ bool knn_gemm_filter_supported(int elem, int row_bytes);
 // block shape of the filter for (element type, row bytes, k): waves per block, query
 // groups per wave, row groups per tile, min waves per SIMD (launch bounds), tile buffers,
 // queries per block, LDS bytes per block
-struct FilterPlan { int nw, qg, rg, minw, nbuf, bm; size_t lds; };
+struct FilterPlan { int nw, qg, rg, minw, nbuf, bm; size_t lds; int kr = 0; /* fused: register-list length */ };
 // kernel-study overrides of the plan (KNN_FILTER_NBUF / KNN_FILTER_SHAPE, read once per
 // context by knn_create); NULL = the product plan
-struct FilterStudy { int nbuf; char shape[8]; int pstep; /* -1 = plan default */ };
+struct FilterStudy {
+    int nbuf; char shape[8]; int pstep; /* -1 = plan default */
+    int kr = -1;      // fused filter: 0 = LDS heaps for every k, -1 = plan default
+};
 FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k, const FilterStudy* fs = nullptr);
 hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st,
                                   const FilterStudy* fs = nullptr);

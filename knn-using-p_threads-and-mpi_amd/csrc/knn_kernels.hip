@@ -71,6 +71,19 @@ __device__ __forceinline__ float direct_dist_batched(const float* q, const E* __
     if ((((uintptr_t)t) & (4 * sizeof(E) - 1)) != 0) return direct_dist(q, t, d);
     float sum = 0.0f;
     int i = 0;
+    for (; i + 64 <= d; i += 64) {  // 16 loads in flight, then the in-order sum over them
+        float4 v[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) v[j] = load4(t + i + 4 * j);
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const int b = i + 4 * j;
+            float d0 = q[b + 0] - v[j].x; sum = sum + d0 * d0;
+            float d1 = q[b + 1] - v[j].y; sum = sum + d1 * d1;
+            float d2 = q[b + 2] - v[j].z; sum = sum + d2 * d2;
+            float d3 = q[b + 3] - v[j].w; sum = sum + d3 * d3;
+        }
+    }
     for (; i + 32 <= d; i += 32) {
         float4 v[8];
 #pragma unroll
@@ -1159,7 +1172,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 //    exist, in ceil(total / 64) ballots per round, and between the wave's smallest and
 //    largest U instead of over all 2^32 values.
 //  * The survivors (L <= threshold) reuse su as their compact index list.
-// LDS per wave: q row [ld_pad] f32 | counts [C] i32 (C <= KNN_VOTE_LDS_MAX_C) | su [64*CAPW]
+// LDS per wave: q row [ld_pad] f32 | counts [C] i32 (C <= KNN_VOTE_LDS_MAX_C) | su [su_cap]
 // ---------------------------------------------------------------------------------
 template <int R, int CAPW, typename E>
 __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
@@ -1195,6 +1208,8 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
         if (lane == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = (int32_t)q;
         return;
     }
+    // the query row into LDS now: its loads overlap the candidate reads below
+    for (int i = lane; i < a.d; i += 64) qs[i] = widen(test[q * a.ld_q + i]);
     const int excl = incl - cs;
     const int64_t qbase = q * (int64_t)a.cap;
     // candidate position of compact entry e: slice = last sg with excl[sg] <= e
@@ -1207,13 +1222,16 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
         return qbase + (int64_t)sg * a.cap_seg + (e - base);
     };
     const int nreg = (total + 63) >> 6;  // <= CAPW (total <= nseg * cap_seg <= cap)
+    // entries e < su_cap are staged in LDS; a longer list (rare: su_cap is sized ~3x the
+    // expected count) re-reads the rest from the candidate arrays in each bisection round
+    const int su_cap = a.su_cap;
     uint32_t umin = 0xffffffffu, umax = 0u;
     for (int i = 0; i < nreg; i++) {
         const int e = lane + 64 * i;
         const int64_t o = position(e);
         if (e < total) {
             const uint32_t u = f2o(a.cand_U[o]);
-            su[e] = u;
+            if (e < su_cap) su[e] = u;
             umin = min(umin, u);
             umax = max(umax, u);
         }
@@ -1234,12 +1252,17 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
         int c = 0;
         for (int i = 0; i < nreg; i++) {
             const int e = lane + 64 * i;
-            c += __popcll(__ballot(e < total && su[e] <= mid));
+            // position() shuffles across the wave: every lane calls it (wave-uniform branch)
+            const int64_t o = 64 * i + 63 >= su_cap ? position(e) : 0;
+            uint32_t u = 0xffffffffu;
+            if (e < total) u = e < su_cap ? su[e] : f2o(a.cand_U[o]);
+            c += __popcll(__ballot(e < total && u <= mid));
         }
         if (c >= k) hi = mid; else lo = mid + 1;
     }
     const float thr = o2f(hi);
-    // compact survivors L <= thr into su (a write never overtakes an unread entry)
+    // compact survivors L <= thr into su (a write never overtakes an unread entry; more
+    // survivors than su holds -- pathological ties -- send the query to the exact scan)
     int m = 0;
     for (int i = 0; i < nreg; i++) {
         const int e = lane + 64 * i;
@@ -1249,10 +1272,14 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
         const u64 bal = __ballot(sv);
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        if (sv) su[m + __popcll(bal & ((1ull << lane) - 1ull))] = (uint32_t)t;
+        const int slot = m + __popcll(bal & ((1ull << lane) - 1ull));
+        if (sv && slot < su_cap) su[slot] = (uint32_t)t;
         m += __popcll(bal);
     }
-    for (int i = lane; i < a.d; i += 64) qs[i] = widen(test[q * a.ld_q + i]);
+    if (m > su_cap) {
+        if (lane == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = (int32_t)q;
+        return;
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
 
@@ -1752,7 +1779,8 @@ static hipError_t launch_rescore_r(const RescoreArgs& a0, hipStream_t st) {
     RescoreArgs a = a0;
     a.q_lds_bytes = (int)align16((size_t)a.d * 4);
     a.c_lds_bytes = a.C <= KNN_VOTE_LDS_MAX_C ? (int)align16((size_t)a.C * 4) : 0;
-    a.wave_lds_bytes = a.q_lds_bytes + a.c_lds_bytes + 64 * KNN_RESCORE_CAPW * 4;
+    a.su_cap = std::max(64, std::min(64 * KNN_RESCORE_CAPW, (a.su_cap + 63) / 64 * 64));
+    a.wave_lds_bytes = a.q_lds_bytes + a.c_lds_bytes + a.su_cap * 4;
     size_t lds = 4 * (size_t)a.wave_lds_bytes;
     unsigned grid = (unsigned)((a.nq + 3) / 4);
     if (grid == 0) return hipSuccess;

@@ -128,6 +128,30 @@ def test_seeded_thresholds(knn, oracle, ctxs, monkeypatch, d, k, nt, nq):
         assert np.array_equal(pred, opred), algo
 
 
+@pytest.mark.parametrize("su", [64, 128])
+def test_rescore_small_staging(knn, oracle, monkeypatch, su):
+    """k_rescore stages about twice the expected candidates per query in LDS; longer lists
+    re-read the rest from the candidate arrays in every bisection round, and more survivors
+    than the staging holds send the query to the exact scan.  KNN_RESCORE_SU (test hook)
+    shrinks the staging so both paths run on most queries: results stay bit-identical."""
+    monkeypatch.setenv("KNN_RESCORE_SU", str(su))
+    for d, k, nt, nq in ((128, 10, 20000, 300), (64, 32, 30000, 200), (128, 100, 9000, 70)):
+        tr, tl = oracle.gen(17, 0, 0, nt, d)
+        te, _ = oracle.gen(17, 1, 0, nq, d)
+        tr[1::5] = tr[0]  # exact ties: long candidate lists, many survivors
+        bad, opred, odist, oidx = oracle.knn(tr, tl, te, k, 10)
+        assert bad == 0
+        for algo in ("gemm", "gemm_bf16", "auto"):
+            ctx = knn.Context(0, algo=algo)
+            try:
+                pred, dist, idx = ctx.predict(tr, tl, te, k, 10, topk=True)
+            finally:
+                ctx.close()
+            assert np.array_equal(idx, oidx), (algo, d, k)
+            assert np.array_equal(dist.view(np.uint32), odist.view(np.uint32)), (algo, d, k)
+            assert np.array_equal(pred, opred), (algo, d, k)
+
+
 @pytest.mark.parametrize("algo", ["gemm_split", "gemm_bf16"])
 @pytest.mark.parametrize("case", ["near_ties", "wide_range", "subnormal", "large"])
 def test_split_operands_stress(knn, oracle, ctxs, case, algo):
