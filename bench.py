@@ -23,7 +23,8 @@ HBM, classified by the direct-form path (k_exact_scan); its predictions are comp
 with the golden file captured from the reference (accuracy bit-match), and the CPU
 baseline is the reference's own multi-thread binary (and serial main) on the same files.
 
-Rank 0 prints one JSON line.  roofline: the dominant kernel (k_gemm_filter) timed with
+Rank 0 prints one JSON line.  roofline: the dominant kernel (k_gemm_fused, the fused-norm
+bf16 filter; k_gemm_filter for the fp32 / split operands) timed with
 HIP events on its own stream; cpu_baseline: the reference's pthreads KNN (oracle/_ref,
 built -O0 as shipped) on a bounded sample, else the C restatement labelled "port".
 """
@@ -264,8 +265,8 @@ def host_buffer_times(knn, local, algo, train, labels, test, k, C, pred_dev):
 
 
 def pmc_traffic(config):
-    """HBM bytes per k_gemm_filter launch from the newest committed rocprofv3 --pmc
-    summary taken on this workload (profiles/*pmc_traffic*.json, key "config")."""
+    """HBM bytes per filter launch from the newest committed rocprofv3 --pmc summary taken on
+    this workload (profiles/*pmc_traffic*.json, key "config")."""
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic*.json")), reverse=True):
         with open(path) as f:
             rec = json.load(f)
@@ -445,7 +446,8 @@ def main():
             roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1),
                     "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                     "traffic": pmc_traffic(args.config + ("" if operands == dtype else PMC_SUFFIX.get(operands, "/" + operands))),
-                    "kernel": "k_gemm_filter", "filter_operands": operands,
+                    "kernel": "k_gemm_fused" if stats.get("fused_norm") else "k_gemm_filter",
+                    "filter_operands": operands,
                     "algorithmic_flops_per_launch": flops, "avg_launch_ms": round(filt_ms, 3)}
             if issued > 1:
                 roof["peak_basis"] = (f"bf16 dense {MFMA_PEAK_TFLOPS['bf16']} TFLOP/s / {issued}: "

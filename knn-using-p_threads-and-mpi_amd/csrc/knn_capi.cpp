@@ -638,6 +638,11 @@ knn_status validate_call(knn_ctx* c, const knn_dataset* tr, const knn_dataset* t
         (((uintptr_t)te->feat) & 15))
         return fail(c, KNN_EINVAL, "device rows must be 16-byte aligned (ld * element size %% 16 == 0)");
     if (te->n > 0 && !shard && !out.pred) return fail(c, KNN_EINVAL, "pred is NULL");
+    // the exact scan (KNN_ALGO_DIRECT_SCAN, and every GEMM path's fallback) stages the query
+    // row in LDS: bound d by it up front instead of failing at a launch
+    if (knn_exact_scan_lds(tr->d, k, C) > 160 * 1024)
+        return fail(c, KNN_EINVAL, "d=%d too wide for the exact scan's LDS query row at k=%d, C=%d (d <= ~%d)",
+                    tr->d, k, C, (int)((160 * 1024 - knn_exact_scan_lds(0, k, C)) / 4));
     return KNN_OK;
 }
 

@@ -12,7 +12,7 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 STEPS=${STEPS:-2}
 cd /tmp && export TMPDIR=/tmp
 OUT=$R/gpurun_out
-BENCH="$R/bench.py --steps $STEPS --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
+BENCH="$R/bench.py --steps $STEPS --warmup 1 --no-cpu-baseline --no-host-path ${BENCH_ARGS:-}"
 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_trace -o run \
     -- python3 $BENCH > $OUT/prof_trace.log 2>&1 || { echo "trace pass failed"; exit 1; }

@@ -56,7 +56,7 @@ def main():
     # the bench workload these counters were taken on (bench.py pmc_traffic(config))
     out = {"tag": tag, "config": sys.argv[3] if len(sys.argv) > 3 else "A"}
     for k, c in counters.items():
-        if "k_gemm_filter" not in k:
+        if "k_gemm_filter" not in k and "k_gemm_fused" not in k:
             continue
         fetch = mean([v for v, _ in c.get("FETCH_SIZE", [])])
         write = mean([v for v, _ in c.get("WRITE_SIZE", [])])

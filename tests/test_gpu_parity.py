@@ -266,6 +266,15 @@ def test_edge_cases(knn, ctxs):
     assert list(c.predict(bad, tl, te, 1, 3)) == [0, 0]
     # empty query set
     assert c.predict(tr, tl, te[:0], 3, 3).shape == (0,)
+    # rows too wide for the exact scan's LDS query row (the fallback of every path): EINVAL
+    # up front, not a failed launch
+    import torch
+    wide = torch.zeros((70, 45000), dtype=torch.float32, device="cuda:0")
+    wl = torch.zeros(70, dtype=torch.int32, device="cuda:0")
+    wp = torch.empty(3, dtype=torch.int32, device="cuda:0")
+    with pytest.raises(knn.KnnError) as e:
+        c.predict_device(wide, wl, wide[:3], 3, 3, wp)
+    assert e.value.status == knn.KNN_EINVAL and "too wide" in str(e.value)
     # k <= 0: all-zero predictions at the Python/C++ surface (reference quirk)
     assert list(knn.KNN((tr, tl), te, 0)) == [0, 0]
 
