@@ -55,9 +55,12 @@ def main():
 
     # the bench workload these counters were taken on (bench.py pmc_traffic(config))
     out = {"tag": tag, "config": sys.argv[3] if len(sys.argv) > 3 else "A"}
-    for k, c in counters.items():
-        if "k_gemm_filter" not in k and "k_gemm_fused" not in k:
-            continue
+    # the filter launch that did the work: the matching kernel with the longest trace time
+    # (AUTO's gated re-run launches the split filter, which exits at once)
+    cands = [k for k in counters if "k_gemm_filter" in k or "k_gemm_fused" in k]
+    cands.sort(key=lambda k: sum(dur.get(k, [0.0])))
+    for k in cands[-1:]:
+        c = counters[k]
         fetch = mean([v for v, _ in c.get("FETCH_SIZE", [])])
         write = mean([v for v, _ in c.get("WRITE_SIZE", [])])
         gui = c.get("GRBM_GUI_ACTIVE", [])
