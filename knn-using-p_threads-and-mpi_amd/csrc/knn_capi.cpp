@@ -61,7 +61,8 @@ struct knn_ctx {
     DBuf tnorm, tnp, qnorm, gthr, cnt, cand_idx, cand_L, cand_U, fb_list, ctrl, timing;
     DBuf split_t, split_q;  // KNN_ALGO_GEMM_SPLIT / _BF16: bf16 [hi | lo] / rn copies of fp32 rows
     DBuf seg_rec;           // k_direct_tile segment records [nseg][nq][3][k]
-    DBuf tmax;              // fused filter: per-64-row maximum train norm
+    DBuf tmax;              // fused filter: per-64-row train stats {max tn, max |t - rt|, max |rt|, 0}
+    DBuf qstat;             // fused filter: per-query {|q|, |q - rq|} upper bounds
     // kernel-study switches, read once from the environment in knn_create (never in a call)
     int study_seed = 0, study_timing = 0, study_nofused = 0;
     int rescore_su = 0;  // test hook KNN_RESCORE_SU: the rescore's LDS staging size (0 = sized)
@@ -314,11 +315,17 @@ void certificate(int d, int felem, float* coef, float* eta) {
 //   fp32 norms (fmaf chains): <= 1.01 d u each, 2.02 d u N;  G's rounding: <= 3.01 u N
 //   the reference's D vs the exact distance: <= 2 (d+2) u N
 // -> (8.04 d + 20.1) u N; the roundings of s, coef s, L and U and slack in 512 u N:
-//   bf16 data: coef = (9d + 512) u.  Rounded fp32 data adds the operand rounding,
-//   2 sum |q_i t_i - rn(q_i) rn(t_i)| <= (2^-7 + 2^-16) N = 131328 u N: coef = (9d + 131840) u.
+//   coef = (9d + 512) u.
+// Rounded fp32 data adds the operand rounding, exactly 2 (q.t - rq.rt) = 2 (q.(t - rt) +
+// (q - rq).rt), bounded by Cauchy-Schwarz with the row statistics of k_row_norms:
+//   |.| <= 2 (|q| |t - rt| + |q - rq| |rt|)   (rq = rn(-2q) / -2, rt = rn(t))
+// -- per (query, 64-row tile) with the tile's maxima, added to Delta by the kernel (tq.y).
+// For random rounding errors it is ~2.6x tighter than the worst case (2^-7 + 2^-16) N
+// (the round-1 coefficient 131328 u); for bf16 data it is 0.  (The terms of the MFMA
+// sum stay <= 2.01 N: |rq_i rt_i| <= (1 + 2^-8)^2 |q_i t_i|.)
 // eta (products or partial sums flushed to zero, subnormal operand rounding): (8d + 16) 2^-125.
-void certificate_fused(int d, bool rounded, float* coef, float* eta) {
-    *coef = (float)(9 * d + (rounded ? 131840 : 512)) * 0x1p-24f;
+void certificate_fused(int d, bool /*rounded*/, float* coef, float* eta) {
+    *coef = (float)(9 * d + 512) * 0x1p-24f;
     *eta = (float)(8 * d + 16) * 0x1p-125f;
 }
 
@@ -381,17 +388,20 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     float coef, eta;
     if (fused) {
         certificate_fused(d, felem == ELEM_ROUND, &coef, &eta);
-        HIP_OR_FAIL(c, c->tmax.ensure(sizeof(float) * ((nt + 63) / 64 + 1)));
+        HIP_OR_FAIL(c, c->tmax.ensure(sizeof(float4) * ((nt + 63) / 64 + 1)));
+        HIP_OR_FAIL(c, c->qstat.ensure(sizeof(float2) * (nq + 1)));
     } else {
         certificate(d, felem, &coef, &eta);
     }
     stage_begin(c, st, gate ? "norms_rerun" : "norms");
     HIP_OR_FAIL(c, knn_launch_row_norms(tr->feat, dtype, nt, tr->ld, d, c->tnorm.as<float>(),
                                         c->ctrl.as<int32_t>(), c->ctrl.as<uint32_t>() + 2,
-                                        c->tnp.as<float>(), 1.0f - coef, st, fused ? c->tmax.as<float>() : nullptr,
+                                        c->tnp.as<float>(), 1.0f - coef, st, fused ? c->tmax.as<float4>() : nullptr,
                                         gate));
+    // (the fused filter's query operand is rn(-2 q): its rounding is bounded for rn(-2 q) / -2)
     HIP_OR_FAIL(c, knn_launch_row_norms(te->feat, dtype, nq, te->ld, d, c->qnorm.as<float>(),
-                                        c->ctrl.as<int32_t>(), nullptr, nullptr, 0.0f, st, nullptr, gate));
+                                        c->ctrl.as<int32_t>(), nullptr, nullptr, 0.0f, st, nullptr, gate,
+                                        fused ? c->qstat.as<float2>() : nullptr, -2.0f));
     stage_end(c, st);
     // (a norm >= 2^125 sets GEMM_UNSAFE in the status word: the filter then skips and the
     // rescore sends every query to the exact fallback scan -- decided on the device)
@@ -467,7 +477,8 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     g.gthr = c->gthr.as<uint32_t>();
     g.cnt = c->cnt.as<int32_t>(); g.cand_idx = c->cand_idx.as<int32_t>();
     g.cand_L = c->cand_L.as<float>(); g.cand_U = c->cand_U.as<float>(); g.cap = cap; g.cap_seg = cap / nseg;
-    g.tmax = fused ? c->tmax.as<float>() : nullptr;
+    g.tstat = fused ? c->tmax.as<float4>() : nullptr;
+    g.qstat = fused ? c->qstat.as<float2>() : nullptr;
     g.status = c->ctrl.as<int32_t>();
     g.gate = gate;
     // kernel studies: KNN_FILTER_TIMING=1 with a -DKNN_FILTER_TIMING build prints the
@@ -594,7 +605,7 @@ void knn_destroy(knn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (DBuf* b : {&c->tnorm, &c->tnp, &c->qnorm, &c->gthr, &c->cnt, &c->cand_idx, &c->cand_L, &c->cand_U,
-                    &c->fb_list, &c->ctrl, &c->timing, &c->split_t, &c->split_q, &c->seg_rec, &c->tmax, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
+                    &c->fb_list, &c->ctrl, &c->timing, &c->split_t, &c->split_q, &c->seg_rec, &c->tmax, &c->qstat, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
                     &c->h_dist, &c->h_idx})
         b->release();
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);

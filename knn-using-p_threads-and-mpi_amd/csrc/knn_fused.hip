@@ -30,6 +30,9 @@
 #ifndef KNN_FUSED_DEFER_EVERY
 #define KNN_FUSED_DEFER_EVERY 64  // tiles between flushes of the deferred queues
 #endif
+#ifndef KNN_FUSED_ROW_NORM
+#define KNN_FUSED_ROW_NORM 0  // 1: the slow path's bounds use each row's norm (an LDS ring filled by DMA)
+#endif
 #ifndef KNN_FUSED_RQ
 #define KNN_FUSED_RQ 4  // deferred-queue depth per lane
 #endif
@@ -123,10 +126,16 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
     constexpr int VPS = (16 + NS - 1) / NS;      // fast-test values per k-step per accumulator
     constexpr int NR = NBUF + 1;                 // norm ring slots: tiles it-1 .. it+NBUF-1
     constexpr int RS = BN;                       // ring slot: BN row norms
-    static_assert(NBUF == 2 || NBUF == 3, "tile buffers");
+    static_assert(NBUF == 2 || NBUF == 3 || NBUF == 4, "tile buffers");
+    // NBUF = 4: tiles go in pairs -- one barrier per two tiles; the DMA of tile it + 2 is
+    // issued during step it into the buffer tile it - 2 used (read before this pair's barrier)
+    constexpr bool PAIR = NBUF == 4;
+    constexpr int AHEAD = PAIR ? 2 : NBUF - 1;  // tiles between a step and the tile it DMAs
     static_assert(RG == 1 || RG == 2, "row groups");
-    static_assert(KR == 0 || KR == 16, "register list length");
-    constexpr bool RL = KR > 0;  // thresholds from per-lane register lists (else LDS heaps)
+    static_assert(KR == 0 || KR == 16 || KR == 32, "register lists: k <= 16, k <= 32, or LDS heaps");
+    constexpr bool RL = KR > 0;       // thresholds from per-lane register lists (else LDS heaps)
+    constexpr bool HALVES = KR == 32;  // k <= 32: one 16-entry list per lane half (below)
+    constexpr int LL = 16;             // register list length
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* tiles = smem;                                     // [NBUF][TILE]
     float* ring = reinterpret_cast<float*>(smem + NBUF * TILE);      // [NR][RS] train norms tn
@@ -178,7 +187,19 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
         tfb = qvalid ? ((thr - qn) + fmaf(coef, qn, eta)) + 0x1p-18f * (fabsf(thr) + qn) : -INF;
     };
     make_tfb();
-    auto tf_of = [&](float tm) __attribute__((always_inline)) { return fmaf(coef + 0x1p-18f, tm, tfb); };
+    // tile term: tq = {the tile's maximum norm tmax, the operand-rounding bound of this query
+    // against the tile's rows, 2 (|q| max|t - rt| + |q - rq| max|rt|) (1 + 2^-17)}
+    auto tf_of = [&](float2 tq) __attribute__((always_inline)) { return fmaf(coef + 0x1p-18f, tq.x, tfb) + tq.y; };
+    float qe2 = 0.0f, eq2 = 0.0f;  // 2 |q| and 2 |q - rq|, rounded up
+    if (qvalid) {
+        const float2 qs = a.qstat[q];
+        qe2 = 2.0f * qs.x * (1.0f + 0x1p-17f);
+        eq2 = 2.0f * qs.y * (1.0f + 0x1p-17f);
+    }
+    auto tile_q = [&](int64_t tile) __attribute__((always_inline)) -> float2 {
+        const float4 t = a.tstat[tile];
+        return make_float2(t.x, fmaf(qe2, t.y, eq2 * t.z));
+    };
 
     const int ntiles = (row_end > row_begin) ? (int)((row_end - row_begin + BN - 1) / BN) : 0;
 
@@ -193,10 +214,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
     }
     // this wave's vector-memory ops per tile: its DMA pieces (+ the norm ring load of the
     // last wave) and the tile-max load
-    int n_dma_wave = (wave == NW - 1) ? 2 : 1;
+    int n_dma_wave = (KNN_FUSED_ROW_NORM && wave == NW - 1) ? 2 : 1;
 #pragma unroll
     for (int i = 0; i < DMA_PER_WAVE; i++) n_dma_wave += (wave + NW * i < DMA_INS) ? 1 : 0;
-    constexpr int NPIECE = DMA_PER_WAVE + 1;
+    constexpr int NPIECE = DMA_PER_WAVE + (KNN_FUSED_ROW_NORM ? 1 : 0);
     const uint32_t lds_tiles = __builtin_amdgcn_readfirstlane(lds_addr(tiles));
     const uint32_t lds_ring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
     struct DmaTile { const unsigned char* src; uint32_t lds, lring; int64_t r0; bool full; };
@@ -238,8 +259,20 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
     // 16c + r of the returned set is 1 iff value r of accumulator c passes (y <= tf) in some
     // lane (one v_cmp per value into an SGPR pair; the scalar ops issue beside the MFMAs --
     // measured faster on A than a v_min3 chain plus a separate pass over the values)
+    constexpr int PF = KNN_FUSED_PF / NACC;  // k-steps of A fragments read ahead
+    uint4 pa[PF], pb[PF];                    // PAIR: the odd step's first fragments, read early
+    auto prefetch = [&](int buf) __attribute__((always_inline)) {
+        const unsigned char* tile = tiles + buf * TILE;
+        const unsigned char* a0p = tile + j * STRIDE + 16 * h;
+        const unsigned char* a1p = tile + ((RG == 2 ? 32 : 0) + j) * STRIDE + 16 * h;
+#pragma unroll
+        for (int s = 0; s < PF && s < NS; s++) {
+            pa[s] = *reinterpret_cast<const uint4*>(a0p + 32 * s);
+            if (RG == 2) pb[s] = *reinterpret_cast<const uint4*>(a1p + 32 * s);
+        }
+    };
     auto step = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int buf, bool dma_on, const DmaTile& dd,
-                    float tf) -> uint32_t {
+                    float tf, bool pre) -> uint32_t {
         const unsigned char* tile = tiles + buf * TILE;
         const unsigned char* a0p = tile + j * STRIDE + 16 * h;
         const unsigned char* a1p = tile + ((RG == 2 ? 32 : 0) + j) * STRIDE + 16 * h;
@@ -249,12 +282,16 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
         float mn[NACC];
 #pragma unroll
         for (int c = 0; c < NACC; c++) mn[c] = INF;
-        constexpr int PF = KNN_FUSED_PF / NACC;
         uint4 xa[NS], xb[NS];
 #pragma unroll
         for (int s = 0; s < PF && s < NS; s++) {
-            xa[s] = *reinterpret_cast<const uint4*>(a0p + 32 * s);
-            if (RG == 2) xb[s] = *reinterpret_cast<const uint4*>(a1p + 32 * s);
+            if (pre) {
+                xa[s] = pa[s];
+                if (RG == 2) xb[s] = pb[s];
+            } else {
+                xa[s] = *reinterpret_cast<const uint4*>(a0p + 32 * s);
+                if (RG == 2) xb[s] = *reinterpret_cast<const uint4*>(a1p + 32 * s);
+            }
         }
 #pragma unroll
         for (int s = 0; s < NS; s++) {
@@ -351,10 +388,14 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
             make_tfb();
         }
     };
-    // certified bounds L <= D <= U of value y of row `row` of tile tp (its norm from the ring)
-    auto bounds = [&](float y, int row, int tp, float& L, float& U) __attribute__((always_inline)) {
+    // certified bounds L <= D <= U of value y of row `row` of tile tp: Delta = coef (qn + tn)
+    // + eta with tn the row's norm (KNN_FUSED_ROW_NORM, from the ring) or, by default, the
+    // tile's maximum norm tm >= tn -- a slightly wider band (still L <= D <= U), and no LDS
+    // read and wait per visited value
+    auto bounds = [&](float y, int row, int tp, float2 tq, float& L, float& U) __attribute__((always_inline)) {
         const float G = qn + y;
-        const float dl = fmaf(coef, qn + ring[(tp % NR) * RS + row], eta);
+        const float tn = KNN_FUSED_ROW_NORM ? ring[(tp % NR) * RS + row] : tq.x;
+        const float dl = fmaf(coef, qn + tn, eta) + tq.y;
         L = G - dl;
         U = G + dl;
     };
@@ -381,7 +422,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
     };
     // immediate slow path: the passing values of tile tp, visited by index; the two lanes
     // of a query take turns (one heap writer at a time)
-    auto slow = [&](floatx16 (&Y)[NACC], int tp, float tf, uint32_t u) {
+    auto slow = [&](floatx16 (&Y)[NACC], int tp, float tf, float2 tq, uint32_t u) {
         const int64_t tbase = row_begin + (int64_t)tp * BN;
         if constexpr (!PSTEP) u = pass_set(Y, tf);
         while (u) {
@@ -397,7 +438,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
                 if (!__ballot(p && h == hh)) continue;
                 if (p && h == hh && t < row_end) {
                     float L, U;
-                    bounds(y, row, tp, L, U);
+                    bounds(y, row, tp, tq, L, U);
                     accept(L, U, t);
                 }
                 sync_roots(hh);
@@ -406,24 +447,36 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
         publish();
     };
 
-    // register-list slow path (KR > 0): both lanes of a query (its two row halves) keep the
-    // same ascending list lst[] of the KR smallest U of the query's kept candidates -- the
-    // first KR - k entries are -inf pads, so lst[KR-1] is the k-th smallest real U, an upper
-    // bound on D_(k) (k rows with D <= U <= it).  Per passing value the two lanes swap their
-    // candidate U (v_permlane32_swap) and both insert both (2 KR v_med3, the multiset and so
-    // the list come out the same in either order): the query's exact k-th smallest, like the
-    // heap, for all 32 queries of the wave at once -- no LDS, no lane takes turns.
-    float lst[RL ? KR : 1];
+    // register-list slow path (KR > 0), k <= 16: both lanes of a query (its two row halves)
+    // keep the same ascending list lst[] of the 16 smallest U of the query's kept candidates
+    // -- the first 16 - k entries are -inf pads, so lst[15] is the k-th smallest real U, an
+    // upper bound on D_(k) (k rows with D <= U <= it).  Per passing value the two lanes swap
+    // their candidate U (v_permlane32_swap) and both insert both (32 v_med3, the multiset and
+    // so the list come out the same in either order): the query's exact k-th smallest, like
+    // the heap, for all 32 queries of the wave at once -- no LDS, no lane takes turns.
+    // HALVES (16 < k <= 32): each lane keeps its own half's ceil(k/2) smallest U (16 - ceil(k/2)
+    // pads) and inserts only its own values (16 v_med3); the bound is the larger of the two
+    // halves' ceil(k/2)-th smallest -- at least 2 ceil(k/2) >= k kept rows have U <= it.  A
+    // little looser than the exact k-th smallest, with no LDS heap and no turn-taking.
+    float lst[RL ? LL : 1];
     if constexpr (RL) {
+        const int pads = LL - (HALVES ? (k + 1) / 2 : k);
 #pragma unroll
-        for (int i = 0; i < KR; i++) lst[i] = i < KR - k ? -INF : INF;
+        for (int i = 0; i < LL; i++) lst[i] = i < pads ? -INF : INF;
     }
     auto list_insert = [&](float w) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = KR - 1; i >= 1; i--) lst[i] = __builtin_amdgcn_fmed3f(lst[i - 1], w, lst[i]);
+        for (int i = LL - 1; i >= 1; i--) lst[i] = __builtin_amdgcn_fmed3f(lst[i - 1], w, lst[i]);
         lst[0] = fminf(lst[0], w);
     };
-    auto slow_rl = [&](floatx16 (&Y)[NACC], int tp, float tf, uint32_t u) {
+    // the other lane half's copy of a word (v_permlane32_swap: one result of the swap is this
+    // lane's own word, the other its partner's)
+    auto partner = [&](float x) __attribute__((always_inline)) -> float {
+        const uint32_t xb = __float_as_uint(x);
+        const auto sw = __builtin_amdgcn_permlane32_swap(xb, xb, false, false);
+        return __uint_as_float(sw[0] == xb ? sw[1] : sw[0]);
+    };
+    auto slow_rl = [&](floatx16 (&Y)[NACC], int tp, float tf, float2 tq, uint32_t u) {
         if constexpr (RL) {
             const int64_t tbase = row_begin + (int64_t)tp * BN;
             if constexpr (!PSTEP) u = pass_set(Y, tf);
@@ -435,18 +488,22 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
                 const int row = 32 * (v >> 4) + (r & 3) + 8 * (r >> 2) + 4 * h;
                 const int64_t t = tbase + row;
                 float L, U;
-                bounds(y, row, tp, L, U);
+                bounds(y, row, tp, tq, L, U);
                 const bool keep = y <= tf && t < row_end && L <= thr;
                 if (keep) store_cand(L, U, t);
-                const float w = (keep && U < lst[KR - 1]) ? U : INF;
-                // one result of the swap is this lane's own word, the other its partner's
-                const uint32_t wb = __float_as_uint(w);
-                const auto sw = __builtin_amdgcn_permlane32_swap(wb, wb, false, false);
-                const float wp = __uint_as_float(sw[0] == wb ? sw[1] : sw[0]);  // the other half's
-                if (__ballot(w < INF || wp < INF)) {
-                    list_insert(w);
-                    list_insert(wp);
-                    thr = fminf(thr, lst[KR - 1]);
+                const float w = (keep && U < lst[LL - 1]) ? U : INF;
+                if constexpr (HALVES) {
+                    if (__ballot(w < INF)) {
+                        list_insert(w);
+                        thr = fminf(thr, fmaxf(lst[LL - 1], partner(lst[LL - 1])));
+                    }
+                } else {
+                    const float wp = partner(w);  // the other half's candidate
+                    if (__ballot(w < INF || wp < INF)) {
+                        list_insert(w);
+                        list_insert(wp);
+                        thr = fminf(thr, lst[LL - 1]);
+                    }
                 }
             }
             make_tfb();
@@ -488,7 +545,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
         tph[7] += __builtin_amdgcn_s_memtime() - tf0;
 #endif
     };
-    auto record = [&](floatx16 (&Y)[NACC], int tp, float tf, uint32_t u) {
+    auto record = [&](floatx16 (&Y)[NACC], int tp, float tf, float2 tq, uint32_t u) {
         const int64_t tbase = row_begin + (int64_t)tp * BN;
         if constexpr (!PSTEP) u = pass_set(Y, tf);
 #ifdef KNN_FILTER_TIMING
@@ -506,7 +563,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
             const int64_t t = tbase + row;
             if (p && t < row_end) {
                 float L, U;
-                bounds(y, row, tp, L, U);
+                bounds(y, row, tp, tq, L, U);
                 if (L <= thr) {
 #pragma unroll
                     for (int i = 0; i < RQ; i++) {
@@ -525,7 +582,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
     for (int c = 0; c < NACC; c++) accA[c] = accB[c] = floatx16{};
     __syncthreads();  // LDS init is complete before any DMA lands
 #pragma unroll
-    for (int p = 0; p < NBUF - 1; p++)
+    for (int p = 0; p < AHEAD; p++)
         if (p < ntiles) dma_tile(p, p, row_begin + (int64_t)p * BN);
 #ifndef KNN_FUSED_EARLY_DMA
 #define KNN_FUSED_EARLY_DMA 0
@@ -534,8 +591,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
     constexpr bool DEFER = NW == 8 && KNN_FUSED_DEFER && !RL;
     constexpr int DEFER_EVERY = KNN_FUSED_DEFER_EVERY;
     // per-64-row maximum train norm of the tile in the pipeline (tile it) and of tile it-1
-    const float* tmaxp = a.tmax + (row_begin >> 6);
-    float tm_prev = 0.0f;
+    const int64_t tile0 = row_begin >> 6;
+    float2 tm_prev = make_float2(0.0f, 0.0f);
+    float2 tm_odd = make_float2(0.0f, 0.0f);  // PAIR: the second tile's term, loaded with the first's
     auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
         if ((it & 63) == 63) {
             if (a.nseg > 1 && qvalid) {
@@ -550,28 +608,49 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
                 if (gv < thr) { thr = gv; make_tfb(); }
             }
         }
-        const bool keep_next = NBUF == 3 && it + 1 < ntiles && (LATE_DMA || !dirty);
         KNN_TSTAMP(t0);
-        wait_dma_barrier(keep_next ? n_dma_wave : 0);
+        if constexpr (PAIR) {
+            // pair (it, it + 1) starts: both tiles have landed (every wave's pieces), and
+            // every wave is done with the previous pair's buffers
+            if ((it & 1) == 0) wait_dma_barrier(0);
+        } else {
+            const bool keep_next = NBUF == 3 && it + 1 < ntiles && (LATE_DMA || !dirty);
+            wait_dma_barrier(keep_next ? n_dma_wave : 0);
+        }
         dirty = false;
         // this tile's maximum train norm, for its fast test in the next iteration: issued after
         // the barrier, it lands under this step (the next barrier's wait covers it)
-        const float tm_cur = tmaxp[(it * BN) >> 6];
+        float2 tm_cur;
+        if constexpr (PAIR) {
+            // both tiles' maxima after the pair's barrier: no compiler wait on a load issued
+            // before the DMA of the second step (it would wait for that DMA too)
+            if ((it & 1) == 0) {
+                tm_cur = tile_q(tile0 + ((it * BN) >> 6));
+                tm_odd = tile_q(tile0 + ((min(it + 1, ntiles - 1) * BN) >> 6));
+            } else {
+                tm_cur = tm_odd;
+            }
+        } else {
+            tm_cur = tile_q(tile0 + ((it * BN) >> 6));
+        }
         KNN_TSTAMP(t1);
 #ifndef KNN_ABLATE_NO_DMA
-        const bool dma_on = it + NBUF - 1 < ntiles;
+        const bool dma_on = it + AHEAD < ntiles;
 #else
         const bool dma_on = false;
 #endif
-        const DmaTile dd = dma_desc((it + NBUF - 1) % NBUF, (it + NBUF - 1) % NR, row_begin + (int64_t)(it + NBUF - 1) * BN);
+        const DmaTile dd = dma_desc((it + AHEAD) % NBUF, (it + AHEAD) % NR, row_begin + (int64_t)(it + AHEAD) * BN);
         const float tf = it > 0 ? tf_of(tm_prev) : -INF;
-        const uint32_t uY = step(X, Y, it % NBUF, dma_on && !LATE_DMA, dd, tf);
+        const uint32_t uY = step(X, Y, it % NBUF, dma_on && !LATE_DMA, dd, tf, PAIR && (it & 1));
+        // PAIR: the odd tile is resident since this pair's barrier -- its first fragments
+        // are read now, so their latency hides under the slow path below
+        if (PAIR && (it & 1) == 0 && it + 1 < ntiles) prefetch((it + 1) % NBUF);
         KNN_TSTAMP(t2);
 #ifndef KNN_ABLATE_NO_SLOW
         if (uY) {
-            if constexpr (RL) { slow_rl(Y, it - 1, tf, uY); dirty = true; }
-            else if constexpr (DEFER) record(Y, it - 1, tf, uY);
-            else { slow(Y, it - 1, tf, uY); dirty = true; }
+            if constexpr (RL) { slow_rl(Y, it - 1, tf, tm_prev, uY); dirty = true; }
+            else if constexpr (DEFER) record(Y, it - 1, tf, tm_prev, uY);
+            else { slow(Y, it - 1, tf, tm_prev, uY); dirty = true; }
         }
         if constexpr (DEFER) {
             if ((it & (DEFER_EVERY - 1)) == DEFER_EVERY - 1 && __ballot(qcnt > 0)) {
@@ -603,9 +682,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
             const float tf = tf_of(tm_prev);
             const uint32_t u = pass_set(Lc, tf);
             if (u) {
-                if constexpr (RL) slow_rl(Lc, last, tf, u);
-                else if constexpr (DEFER) record(Lc, last, tf, u);
-                else slow(Lc, last, tf, u);
+                if constexpr (RL) slow_rl(Lc, last, tf, tm_prev, u);
+                else if constexpr (DEFER) record(Lc, last, tf, tm_prev, u);
+                else slow(Lc, last, tf, tm_prev, u);
             }
         };
         if (last & 1) drain(accB);
@@ -651,14 +730,15 @@ bool knn_fused_supported(int d) { return d == 64 || d == 128 || d == 256; }
 //            barrier and fast test outweigh 5 MFMAs per 32x32 block; the other block hides them)
 //  d >= 128: 8 waves x 32 queries (two waves per SIMD), 64-row tiles, double-buffered; 32-row
 //            tiles when the per-query heaps of a large k leave no room for 64-row tiles.
-// Thresholds: k <= 16 keeps per-query register lists (KR = 16), larger k the LDS heaps
-// (measured on B, k = 32: 32-entry lists cost a block per CU of occupancy and 9 % of time).
+// Thresholds: k <= 16 keeps per-query register lists (KR = 16), k <= 32 per-half lists
+// (KR = 32, 16 entries: exact 32-entry lists cost a block per CU of occupancy and 9 % of
+// time on B), larger k the LDS heaps.
 FilterPlan knn_fused_plan(int d, int k, const FilterStudy* fs) {
     const int rb = 2 * d + 32;
     const size_t cap = 160 * 1024 - 256;  // room for the kernel's static LDS (the start tile)
-    // pass-set variant (FilterPlan.qg): in-step for d >= 128; KNN_FILTER_PSTEP overrides (study)
-    const int pstep = fs && fs->pstep >= 0 ? fs->pstep : (d >= 128 ? 1 : 0);
-    int kr = k <= 16 ? 16 : 0;
+    // pass-set variant (FilterPlan.qg): in-step for d >= 128 (measured; fused_fn)
+    const int pstep = d >= 128 ? 1 : 0;
+    int kr = k <= 16 ? 16 : k <= 32 ? 32 : 0;
     if (fs && fs->kr == 0) kr = 0;  // study: the heaps for every k
     auto make = [&](int nw, int rg, int minw, int nbuf) {
         FilterPlan f{nw, pstep, rg, minw, nbuf, 32 * nw, fused_lds_of(rb, k, nw, rg, nbuf, kr == 0)};
@@ -666,9 +746,13 @@ FilterPlan knn_fused_plan(int d, int k, const FilterStudy* fs) {
         return f;
     };
     const bool force8 = fs && fs->shape[0] == 'w' && fs->shape[1] == '8';
-    const int nb = fs && fs->nbuf == 3 ? 3 : 2;  // kernel study: triple-buffered tiles
+    const int nb = fs && (fs->nbuf == 3 || fs->nbuf == 4) ? fs->nbuf : 2;  // kernel study: 3 buffers, or pairs (4)
     const bool force4 = fs && fs->shape[0] == 'w' && fs->shape[1] == '4';
     if ((d == 64 || force4) && !force8 && fused_lds_of(rb, k, 4, 2, nb, kr == 0) <= cap / 2) return make(4, 2, 2, nb);
+    // d >= 128: tiles in pairs (one barrier per two tiles) when four buffers fit -- measured
+    // on A (same box): filter 33.4 -> 31.3 ms; B's d = 64 shape loses occupancy with them
+    const bool study_nb = fs && fs->nbuf > 0;
+    if (!study_nb && fused_lds_of(rb, k, 8, 2, 4, kr == 0) <= cap) return make(8, 2, 2, 4);
     if (fused_lds_of(rb, k, 8, 2, nb, kr == 0) <= cap) return make(8, 2, 2, nb);
     if (fused_lds_of(rb, k, 8, 1, 2, kr == 0) <= cap) return make(8, 1, 2, 2);
     return FilterPlan{0, 0, 0, 0, 0, 0, 0};  // k too large for the LDS heaps: not supported
@@ -681,18 +765,18 @@ FilterPlan knn_fused_plan(int d, int k, const FilterStudy* fs) {
 template <int RB, bool P, int KR>
 static const void* fused_fn_p(const FilterPlan& f) {
 #define KNN_FUSED_FN(NB, NW, RG) reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, NB, NW, RG, P, KR>)
-    if (f.nw == 4) return f.nbuf == 3 ? KNN_FUSED_FN(3, 4, 2) : KNN_FUSED_FN(2, 4, 2);
-    if (f.rg == 2) return f.nbuf == 3 ? KNN_FUSED_FN(3, 8, 2) : KNN_FUSED_FN(2, 8, 2);
+    if (f.nw == 4) return f.nbuf == 4 ? KNN_FUSED_FN(4, 4, 2) : f.nbuf == 3 ? KNN_FUSED_FN(3, 4, 2) : KNN_FUSED_FN(2, 4, 2);
+    if (f.rg == 2) return f.nbuf == 4 ? KNN_FUSED_FN(4, 8, 2) : f.nbuf == 3 ? KNN_FUSED_FN(3, 8, 2) : KNN_FUSED_FN(2, 8, 2);
     return KNN_FUSED_FN(2, 8, 1);
 #undef KNN_FUSED_FN
 }
 template <int RB, bool P>
 static const void* fused_fn_k(const FilterPlan& f) {
-    return f.kr == 16 ? fused_fn_p<RB, P, 16>(f) : fused_fn_p<RB, P, 0>(f);
+    return f.kr == 16 ? fused_fn_p<RB, P, 16>(f) : f.kr == 32 ? fused_fn_p<RB, P, 32>(f) : fused_fn_p<RB, P, 0>(f);
 }
 template <int RB>
 static const void* fused_fn(const FilterPlan& f) {
-    return f.qg ? fused_fn_k<RB, true>(f) : fused_fn_k<RB, false>(f);
+    return fused_fn_k<RB, (RB >= 288)>(f);  // the pass-set variant follows d (knn_fused_plan)
 }
 
 static const void* fused_ptr(int d, const FilterPlan& f) {
@@ -707,7 +791,7 @@ hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu, const FilterStu
 
 hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st, const FilterStudy* fs) {
     const FilterPlan f = knn_fused_plan(a.d, a.k, fs);
-    if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != a.d + 16 || a.ld_q != a.d + 16 || !a.tmax)
+    if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != a.d + 16 || a.ld_q != a.d + 16 || !a.tstat || !a.qstat)
         return hipErrorInvalidValue;
     void* args[] = {const_cast<GemmFilterArgs*>(&a)};
     const dim3 grid((unsigned)(a.n_qtiles * a.nseg));

@@ -49,7 +49,8 @@ struct GemmFilterArgs {
     unsigned long long* timing;  // KNN_FILTER_TIMING builds: per-phase shader clocks (else NULL)
     int32_t* cnt;  // [nseg][nq] kept rows per (segment, query)
     int32_t* cand_idx; float* cand_L; float* cand_U; int cap; int cap_seg;
-    const float* tmax;  // fused filter: per-64-row maximum train norm
+    const float4* tstat;  // fused filter, per 64-row tile: {max tn, max |t - rt|, max |rt|, 0}
+    const float2* qstat;  // fused filter, per query: {|q|, |q - rq|} upper bounds (rq: the operand / -2)
     const int32_t* status;  // the call's status word: a set GEMM_UNSAFE bit skips the filter
     const int32_t* gate;    // optional: the filter runs only when *gate != 0 (AUTO's re-run)
 };
@@ -114,11 +115,15 @@ struct GenerateArgs {
 
 hipError_t knn_launch_exact_scan(const ExactScanArgs& a, int grid, hipStream_t st);
 size_t knn_exact_scan_lds(int d, int k, int C);
-// tmax (optional): the maximum norm of every 64-row tile, [ceil(n / 64)] (the fused filter)
+// tstat (optional, train rows of the fused filter): per 64-row tile [ceil(n / 64)]
+//   {max ||x||^2, max ||x - rx||, max ||rx||, 0}, rx = rn_bf16(x) (upper bounds)
+// qstat (optional, query rows of the fused filter): per row {||x||, ||x - rx||} upper bounds,
+//   rx = rn_bf16(oscale x) / oscale (the operand the filter multiplies, unscaled)
 // gate (optional): the stage runs only when *gate != 0 (device-side control of AUTO's re-run)
 hipError_t knn_launch_row_norms(const void* x, int elem, int64_t n, int ld, int d, float* out,
                                 int32_t* status, uint32_t* maxo, float* outp, float c1, hipStream_t st,
-                                float* tmax = nullptr, const int32_t* gate = nullptr);
+                                float4* tstat = nullptr, const int32_t* gate = nullptr,
+                                float2* qstat = nullptr, float oscale = 1.0f);
 // row_bytes = d * element size: 128, 256 or 512
 bool knn_gemm_filter_supported(int elem, int row_bytes);
 // block shape of the filter for (element type, row bytes, k): waves per block, query

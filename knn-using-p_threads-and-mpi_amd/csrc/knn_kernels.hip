@@ -199,7 +199,7 @@ __device__ void finish_query(const u64 (&T)[R], int k, int C, const int32_t* __r
     }
     if (lane == 0) {
         o.pred[q] = bad ? 0 : (int32_t)(0xffffffffu - (uint32_t)(best & 0xffffffffull));
-        if (bad) atomicOr(status, KNN_STATUS_TOO_FEW);
+        if (bad && !KNN_STUDY_RESULTS_INVALID) atomicOr(status, KNN_STATUS_TOO_FEW);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -444,44 +444,67 @@ __global__ __launch_bounds__(64 * DT_NW, 4) void k_direct_tile(DirectTileArgs a)
 // k_row_norms: out[r] = sum_i x[r][i]^2 (fp32).  Flags rows whose norm is too large
 // for the GEMM form's error certificate (>= 2^125) so the host falls back, and keeps
 // the maximum norm (ordered bits, atomicMax) for the filter's conservative fast test.
+// For the fused bf16 filter it also bounds the operand rounding (DESIGN.md
+// "Certificate"): with rx = rn_bf16(oscale x) / oscale, sqrt-of-sum upper bounds of
+// ||x - rx|| and ||rx|| (x - rx is exact in fp32): per query row (qstat) or per 64-row
+// tile maximum (tstat).
 // ---------------------------------------------------------------------------------
+// sqrt of an fmaf sum of d squares, rounded up: the sum errs by <= d u (relative), the
+// squares below 2^-150 that flushed add <= d 2^-149; the factor covers d <= 8000
+__device__ __forceinline__ float norm_ub(float s, int d) {
+    return sqrtf(fmaf((float)d, 0x1p-149f, s)) * (1.0f + 0x1p-12f);
+}
 template <typename E>
 __global__ __launch_bounds__(256) void k_row_norms(const E* __restrict__ x, int64_t n, int ld,
                                                    int d, float* __restrict__ out,
                                                    int32_t* __restrict__ status,
                                                    uint32_t* __restrict__ maxo,
                                                    float* __restrict__ outp, float c1,
-                                                   float* __restrict__ tmax, const int32_t* __restrict__ gate) {
+                                                   float4* __restrict__ tstat, const int32_t* __restrict__ gate,
+                                                   float2* __restrict__ qstat, float oscale) {
     if (gate && *gate == 0) return;  // a gated stage (AUTO's re-run) that is not taken
     // rows [n, n + 64) of out/outp get +inf: the GEMM filter's tile tail reads them
     int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    float s = 0.0f;
+    float s = 0.0f, se = 0.0f, sr = 0.0f;
+    const bool rstat = tstat || qstat;
+    const float inv = 1.0f / oscale;  // 1 or -0.5: exact
+    auto acc = [&](float v) __attribute__((always_inline)) {
+        s = fmaf(v, v, s);
+        if (rstat) {
+            const float rv = __uint_as_float(bf16_rne(oscale * v) << 16) * inv;
+            const float e = v - rv;
+            se = fmaf(e, e, se);
+            sr = fmaf(rv, rv, sr);
+        }
+    };
     if (r < n) {
         const E* row = x + r * ld;
         int i = 0;
         for (; i + 4 <= d; i += 4) {
             const float4 v = load4(row + i);
-            s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
+            acc(v.x); acc(v.y); acc(v.z); acc(v.w);
         }
-        for (; i < d; i++) {
-            const float v = widen(row[i]);
-            s = fmaf(v, v, s);
-        }
+        for (; i < d; i++) acc(widen(row[i]));
         out[r] = s;
+        if (qstat) qstat[r] = make_float2(norm_ub(s, d), norm_ub(se, d));
         if (outp) outp[r] = c1 * s;
         if (!(s < 0x1p125f)) atomicOr(status, KNN_STATUS_GEMM_UNSAFE);
     } else if (outp && r < n + 64) {
         out[r] = __uint_as_float(0x7f800000u);
         outp[r] = __uint_as_float(0x7f800000u);
     }
-    if (maxo || tmax) {
+    if (maxo || tstat) {
         // the wave's 64 rows are one 64-row tile of the fused filter (rows >= n count as 0)
-        float m = s;
+        float m = s, me = r < n ? norm_ub(se, d) : 0.0f, mr = r < n ? norm_ub(sr, d) : 0.0f;
 #pragma unroll
-        for (int j = 32; j > 0; j >>= 1) m = fmaxf(m, __shfl_xor(m, j));
+        for (int j = 32; j > 0; j >>= 1) {
+            m = fmaxf(m, __shfl_xor(m, j));
+            me = fmaxf(me, __shfl_xor(me, j));
+            mr = fmaxf(mr, __shfl_xor(mr, j));
+        }
         if ((threadIdx.x & 63) == 0) {
             if (maxo) atomicMax(maxo, f2o(m));
-            if (tmax && r < n) tmax[r >> 6] = m;
+            if (tstat && r < n) tstat[r >> 6] = make_float4(m, me, mr, 0.0f);
         }
     }
 }
@@ -1403,7 +1426,7 @@ __global__ __launch_bounds__(256) void k_merge_vote(MergeArgs a) {
     }
     if (lane == 0) {
         o.pred[q] = bad ? 0 : (int32_t)(0xffffffffu - (uint32_t)(best & 0xffffffffull));
-        if (bad) atomicOr(a.status, KNN_STATUS_TOO_FEW);
+        if (bad && !KNN_STUDY_RESULTS_INVALID) atomicOr(a.status, KNN_STATUS_TOO_FEW);
     }
 }
 
@@ -1643,16 +1666,16 @@ hipError_t knn_launch_direct_tile(DirectTileArgs a, hipStream_t st) {
 
 hipError_t knn_launch_row_norms(const void* x, int elem, int64_t n, int ld, int d, float* out,
                                 int32_t* status, uint32_t* maxo, float* outp, float c1, hipStream_t st,
-                                float* tmax, const int32_t* gate) {
+                                float4* tstat, const int32_t* gate, float2* qstat, float oscale) {
     if (n <= 0) return hipSuccess;
     const int64_t rows = n + (outp ? 64 : 0);
     dim3 grid((unsigned)((rows + 255) / 256));
     if (elem == ELEM_BF16)
         hipLaunchKernelGGL(k_row_norms<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, n, ld, d, out,
-                           status, maxo, outp, c1, tmax, gate);
+                           status, maxo, outp, c1, tstat, gate, qstat, oscale);
     else
         hipLaunchKernelGGL(k_row_norms<float>, grid, dim3(256), 0, st, (const float*)x, n, ld, d, out,
-                           status, maxo, outp, c1, tmax, gate);
+                           status, maxo, outp, c1, tstat, gate, qstat, oscale);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }

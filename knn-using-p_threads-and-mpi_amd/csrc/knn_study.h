@@ -9,7 +9,10 @@
     do {                               \
         if (qlist) return;             \
     } while (0)
+// ... and a query left with fewer than k rows is not an error there
+#define KNN_STUDY_RESULTS_INVALID 1
 #else
+#define KNN_STUDY_RESULTS_INVALID 0
 #define KNN_STUDY_SKIP_FALLBACK(qlist) \
     do {                               \
     } while (0)

@@ -74,7 +74,9 @@ def test_query_range(ctxs, arff):
 
 @pytest.mark.parametrize("d,k,nt,nq", [(128, 10, 20000, 300), (64, 32, 30000, 200), (100, 5, 9000, 257),
                                        (128, 1, 5000, 130), (40, 100, 12000, 64), (128, 128, 8192, 70),
-                                       (32, 3, 70001, 129), (64, 100, 20000, 100), (128, 10, 64, 5)])
+                                       (32, 3, 70001, 129), (64, 100, 20000, 100), (128, 10, 64, 5),
+                                       # 16 < k <= 32: the fused filter's per-half register lists
+                                       (256, 17, 20000, 96), (128, 31, 30000, 128), (64, 24, 40000, 100)])
 def test_synthetic_vs_oracle(knn, oracle, ctxs, d, k, nt, nq):
     tr, tl = oracle.gen(7, 0, 0, nt, d)
     te, _ = oracle.gen(7, 1, 0, nq, d)
@@ -188,6 +190,37 @@ def test_split_operands_stress(knn, oracle, ctxs, case, algo):
         assert np.array_equal(idx, oidx), (case, k)
         assert np.array_equal(dist.view(np.uint32), odist.view(np.uint32)), (case, k)
         assert np.array_equal(pred, opred), (case, k)
+
+
+@pytest.mark.parametrize("d", [64, 128, 256])
+def test_rounded_filter_aligned_rounding(knn, oracle, ctxs, d):
+    """The worst case of the rounded filter's operand-rounding term (DESIGN.md
+    "Certificate"): every element sits just below a bf16 rounding midpoint, so every
+    rounding error has the same sign and q.(t - rt) reaches the Cauchy-Schwarz bound
+    |q| |t - rt| the certificate charges -- while the coarse bf16 grid under the elements
+    keeps the distances spread, so the band (not an overflow) decides which rows are kept.
+    Every true neighbour must survive: results bit-identical to the oracle."""
+    rng = np.random.default_rng(31 + d)
+    nt, nq = 20000, 96
+
+    def rows(n):
+        s = 2.0 ** rng.integers(0, 4, size=(n, d))                # binades [1, 16): spread distances
+        m = 1.0 + rng.integers(0, 128, size=(n, d)) / 128.0      # bf16-exact grid in [1, 2)
+        delta = rng.integers(1, 64, size=(n, d)) * 2.0 ** -22     # stay below the midpoint
+        return ((m + 2.0 ** -8 - delta) * s).astype(np.float32)   # rounds down to m s
+
+    tr, te = rows(nt), rows(nq)
+    tl = rng.integers(0, 10, size=nt).astype(np.int32)
+    for k in (1, 10, 33):
+        bad, opred, odist, oidx = oracle.knn(tr, tl, te, k, 10)
+        assert bad == 0
+        pred, dist, idx = ctxs["gemm_bf16"].predict(tr, tl, te, k, 10, topk=True)
+        st = ctxs["gemm_bf16"].stats()
+        assert st["filter_operands"] == GEMM_OPERANDS["gemm_bf16"] and st["fused_norm"], st
+        assert st["fallback_queries"] < nq // 4, st  # the band, not the fallback, decides
+        assert np.array_equal(idx, oidx), (d, k)
+        assert np.array_equal(dist.view(np.uint32), odist.view(np.uint32)), (d, k)
+        assert np.array_equal(pred, opred), (d, k)
 
 
 @pytest.mark.parametrize("case", ["near_ties", "uniform"])
