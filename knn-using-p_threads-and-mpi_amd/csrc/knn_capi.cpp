@@ -329,6 +329,19 @@ void certificate_fused(int d, bool /*rounded*/, float* coef, float* eta) {
     *eta = (float)(8 * d + 16) * 0x1p-125f;
 }
 
+// the most train segments (or schedule pieces) per query tile whose expected kept rows fit
+// their slice of the candidate list (choose_splits' rule)
+int max_splits(int64_t nt, int k, int cap) {
+    int best = 1;
+    for (int s = 2; s <= 8; s++) {
+        const double rows = (double)nt / s;
+        const double expect = k * (1.0 + std::log(std::max(rows / k, 1.0))) + 64.0;
+        if (1.5 * (0.5 * expect + 32.0) > (double)(cap / s / 2)) break;
+        best = s;
+    }
+    return best;
+}
+
 int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int rb, int k, int cap,
                   bool fused = false, int d = 0) {
     if (c->train_splits > 0) return std::min(8, c->train_splits);
@@ -464,15 +477,29 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
 
     const FilterPlan plan = fused ? knn_fused_plan(d, k, &c->fstudy) : knn_gemm_filter_plan(kelem, rb, k, &c->fstudy);
     const int64_t n_qtiles = (nq + plan.bm - 1) / plan.bm;
-    const int nseg = choose_splits(c, n_qtiles, nt, kelem, rb, k, cap, fused, d);
+    GemmFilterArgs g{};
+    g.nt = nt; g.n_qtiles = (int)n_qtiles;
+    // fused filter: the balanced schedule (knn_fused_schedule) when its pieces per query tile
+    // fit the candidate list like segments do; else (or with explicit train_splits) segments
+    int nseg = 0;
+    if (fused && c->train_splits <= 0) {
+        int occ = 1;
+        if (knn_fused_occupancy(d, k, &occ, &c->fstudy) != hipSuccess || occ < 1) occ = 1;
+        int nb = 1;
+        knn_fused_schedule(g, occ * c->num_cus, &nb);
+        if (nb <= max_splits(nt, k, cap)) nseg = nb;
+    }
+    if (nseg == 0) {
+        nseg = choose_splits(c, n_qtiles, nt, kelem, rb, k, cap, fused, d);
+        g.g2 = -1;  // segment schedule
+    }
     int64_t seg_len = (nt + nseg - 1) / nseg;
     seg_len = (seg_len + 63) / 64 * 64;
-    GemmFilterArgs g{};
     g.train = ftrain; g.nt = nt; g.ld_t = fld_t;
     g.test = ftest; g.nq = nq; g.ld_q = fld_q; g.d = d;
     g.tnorm = c->tnorm.as<float>(); g.tnp = c->tnp.as<float>(); g.qnorm = c->qnorm.as<float>();
     g.tnmax = c->ctrl.as<uint32_t>() + 2;
-    g.k = k; g.seg_len = seg_len; g.nseg = nseg; g.n_qtiles = (int)n_qtiles;
+    g.k = k; g.seg_len = seg_len; g.nseg = nseg;
     g.coef = coef; g.eta = eta;
     g.gthr = c->gthr.as<uint32_t>();
     g.cnt = c->cnt.as<int32_t>(); g.cand_idx = c->cand_idx.as<int32_t>();
@@ -489,6 +516,8 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         HIP_OR_FAIL(c, hipMemsetAsync(c->timing.p, 0, 16 * sizeof(unsigned long long), st));
         g.timing = c->timing.as<unsigned long long>();
     }
+    if (fused && g.g2 >= 0 && nseg > 1)  // whole query tiles write only sub-slice 0
+        HIP_OR_FAIL(c, hipMemsetAsync(c->cnt.p, 0, sizeof(int32_t) * 2 * nseg * nq, st));
     stage_begin(c, st, gate ? "gemm_filter_rerun" : "gemm_filter");
     if (fused) HIP_OR_FAIL(c, knn_launch_fused(g, st, &c->fstudy));
     else HIP_OR_FAIL(c, knn_launch_gemm_filter(g, kelem, rb, st, &c->fstudy));

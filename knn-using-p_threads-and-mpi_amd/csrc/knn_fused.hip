@@ -30,6 +30,12 @@
 #ifndef KNN_FUSED_DEFER_EVERY
 #define KNN_FUSED_DEFER_EVERY 64  // tiles between flushes of the deferred queues
 #endif
+#ifndef KNN_FUSED_PSTEP
+#define KNN_FUSED_PSTEP 0  // 1 (study): the in-step pass set for d >= 128
+#endif
+#ifndef KNN_FUSED_PRIO
+#define KNN_FUSED_PRIO 0  // 1 (study): s_setprio 1 for the second half of the waves
+#endif
 #ifndef KNN_FUSED_ROW_NORM
 #define KNN_FUSED_ROW_NORM 0  // 1: the slow path's bounds use each row's norm (an LDS ring filled by DMA)
 #endif
@@ -114,9 +120,11 @@ hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int ld, int d
 // max-heap in LDS, as k_gemm_filter), or a smaller bound published by another segment
 // (gthr).  Every row of the exact top-k has L <= D <= D_(k) <= thr, so it is kept.
 // ---------------------------------------------------------------------------------
-template <int RB, int MINW, int NBUF, int NW, int RG, bool PSTEP, int KR>
-__global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) {
-    if ((a.gate && *a.gate == 0) || (*a.status & KNN_STATUS_GEMM_UNSAFE)) return;  // not taken / exact path
+// fused_piece: one piece of work -- query tile qt against train rows [row_begin, row_end),
+// piece (segment) id seg of that query tile (its candidate sub-slices, 2 seg + h)
+template <int RB, int NBUF, int NW, int RG, bool PSTEP, int KR>
+__device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int qt, const int seg,
+                                            const int64_t row_begin, const int64_t row_end) {
     typedef FilterTile<RB, NW, 1, RG> FT;
     constexpr int NACC = RG, BN = FT::BN, BM = FT::BM, STRIDE = FT::STRIDE, SLOTS = FT::SLOTS;
     constexpr int DMA_INS = FT::DMA_INS, TILE = FT::TILE;
@@ -147,10 +155,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int j = lane & 31;
     const int h = lane >> 5;
-    const int qt = blockIdx.x % a.n_qtiles;
-    const int seg = blockIdx.x / a.n_qtiles;
-    const int64_t row_begin = (int64_t)seg * a.seg_len;
-    const int64_t row_end = min(a.nt, row_begin + a.seg_len);
+    if (KNN_FUSED_PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
     const int k = a.k;
     const float INF = __uint_as_float(0x7f800000u);
     const float coef = a.coef, eta = a.eta;
@@ -714,6 +719,80 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
 #undef KNN_TSTAMP
 }
 
+// The grid (knn_fused_schedule): blocks [0, p1) take one whole query tile each (qt = block,
+// every train row) -- whole rounds of the resident blocks, all sweeping the train rows from
+// row 0 together (one L2 stream per XCD); the remaining query tiles' (qtile, 64-row tile)
+// work is one linear space of w2 units cut into g2 equal ranges, one per block [p1, p1+g2):
+// a range covers the tail of one query tile and the head of the next (a piece each), so the
+// last round of blocks ends together instead of a partial wave of whole query tiles.
+// Pieces of one query tile share thresholds through gthr like segments (piece id = block -
+// the first block of that query tile).  One call site of fused_piece (instruction cache).
+template <int RB, int MINW, int NBUF, int NW, int RG, bool PSTEP, int KR>
+__global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) {
+    if ((a.gate && *a.gate == 0) || (*a.status & KNN_STATUS_GEMM_UNSAFE)) return;  // not taken / exact path
+    const int64_t T = a.tiles64;  // 64-row units per query tile
+    const int b = blockIdx.x;
+    // g2 < 0: segment mode -- block = (segment b / n_qtiles, query tile b % n_qtiles), one piece
+    const bool segmode = a.g2 < 0;
+    const bool p1 = !segmode && b < a.p1_blocks;
+    const int64_t b2 = b - a.p1_blocks;
+    auto lo = [&](int64_t bb) { return bb * a.w2 / a.g2; };
+    int64_t x = 0, x1 = 1;
+    if (!segmode) {
+        x = p1 ? (int64_t)b * T : lo(b2);
+        x1 = p1 ? x + T : lo(b2 + 1);
+    }
+    const int qbase = p1 ? 0 : a.p1_blocks;
+    for (bool first = true; x < x1; first = false) {
+        int qt, seg;
+        int64_t rb, re, adv;
+        if (segmode) {
+            qt = b % a.n_qtiles;
+            seg = b / a.n_qtiles;
+            rb = (int64_t)seg * a.seg_len;
+            re = min(a.nt, rb + a.seg_len);
+            adv = 1;
+        } else {
+            const int64_t ql = x / T, t0 = x - ql * T;
+            const int64_t t1 = min(T, t0 + (x1 - x));
+            qt = qbase + (int)ql;
+            // the block whose range holds the query tile's first unit: largest bb with lo(bb) <= ql T
+            seg = p1 ? 0 : (int)(b2 - ((ql * T + 1) * a.g2 - 1) / a.w2);
+            rb = t0 * 64;
+            re = min(a.nt, t1 * 64);
+            adv = t1 - t0;
+        }
+        if (!first) __syncthreads();  // every wave is done with the previous piece's LDS
+        fused_piece<RB, NBUF, NW, RG, PSTEP, KR>(a, qt, seg, rb, re);
+        x += adv;
+    }
+}
+
+// Balanced schedule (see k_gemm_fused): whole rounds of query tiles, the rest cut into g2 equal
+// ranges of 64-row units (at least min(T, 256) units each).  Returns the grid and sets *nseg
+// to the most pieces one query tile gets (its candidate sub-slices).
+int knn_fused_schedule(GemmFilterArgs& a, int slots, int* nseg) {
+    const int64_t T = (a.nt + 63) / 64;
+    const int64_t nqt = a.n_qtiles;
+    a.tiles64 = T;
+    const int64_t R = nqt / slots, r = nqt - R * slots;
+    a.p1_blocks = (int)(R * slots);
+    *nseg = 1;
+    if (r == 0) {
+        a.g2 = 0;  // whole rounds only
+        a.w2 = 0;
+        return a.p1_blocks;
+    }
+    const int64_t W = r * T;
+    const int64_t minp = std::min<int64_t>(T, 256);
+    const int64_t g2 = std::max<int64_t>(1, std::min<int64_t>(slots, W / minp));
+    a.g2 = (int)g2;
+    a.w2 = W;
+    auto blk = [&](int64_t xx) { return ((xx + 1) * g2 - 1) / W; };
+    for (int64_t ql = 0; ql < r; ql++) *nseg = std::max<int>(*nseg, (int)(blk((ql + 1) * T - 1) - blk(ql * T) + 1));
+    return a.p1_blocks + (int)g2;
+}
+
 // ---------------------------------------------------------------------------------
 // plan and launch
 // ---------------------------------------------------------------------------------
@@ -736,8 +815,9 @@ bool knn_fused_supported(int d) { return d == 64 || d == 128 || d == 256; }
 FilterPlan knn_fused_plan(int d, int k, const FilterStudy* fs) {
     const int rb = 2 * d + 32;
     const size_t cap = 160 * 1024 - 256;  // room for the kernel's static LDS (the start tile)
-    // pass-set variant (FilterPlan.qg): in-step for d >= 128 (measured; fused_fn)
-    const int pstep = d >= 128 ? 1 : 0;
+    // pass-set variant (FilterPlan.qg): the v_min3 chain and a lazy pass set for every d --
+    // measured on A (same box, with the rounding certificate): 29.8 (in-step set) -> 28.8 ms
+    const int pstep = (d >= 128 && KNN_FUSED_PSTEP) ? 1 : 0;
     int kr = k <= 16 ? 16 : k <= 32 ? 32 : 0;
     if (fs && fs->kr == 0) kr = 0;  // study: the heaps for every k
     auto make = [&](int nw, int rg, int minw, int nbuf) {
@@ -748,7 +828,10 @@ FilterPlan knn_fused_plan(int d, int k, const FilterStudy* fs) {
     const bool force8 = fs && fs->shape[0] == 'w' && fs->shape[1] == '8';
     const int nb = fs && (fs->nbuf == 3 || fs->nbuf == 4) ? fs->nbuf : 2;  // kernel study: 3 buffers, or pairs (4)
     const bool force4 = fs && fs->shape[0] == 'w' && fs->shape[1] == '4';
-    if ((d == 64 || force4) && !force8 && fused_lds_of(rb, k, 4, 2, nb, kr == 0) <= cap / 2) return make(4, 2, 2, nb);
+    // d = 64 with register lists: 8-wave blocks in pairs like d >= 128 (B, same box: 765 ms
+    // with 4-wave blocks in pairs, 743 with 8-wave) -- 256 queries share each tile's DMA
+    if ((d == 64 || force4) && !force8 && kr == 0 && fused_lds_of(rb, k, 4, 2, nb, true) <= cap / 2) return make(4, 2, 2, nb);
+    if (force4 && fused_lds_of(rb, k, 4, 2, nb, kr == 0) <= cap / 2) return make(4, 2, 2, nb);
     // d >= 128: tiles in pairs (one barrier per two tiles) when four buffers fit -- measured
     // on A (same box): filter 33.4 -> 31.3 ms; B's d = 64 shape loses occupancy with them
     const bool study_nb = fs && fs->nbuf > 0;
@@ -776,7 +859,7 @@ static const void* fused_fn_k(const FilterPlan& f) {
 }
 template <int RB>
 static const void* fused_fn(const FilterPlan& f) {
-    return fused_fn_k<RB, (RB >= 288)>(f);  // the pass-set variant follows d (knn_fused_plan)
+    return fused_fn_k<RB, (RB >= 288) && KNN_FUSED_PSTEP>(f);  // the pass-set variant (knn_fused_plan)
 }
 
 static const void* fused_ptr(int d, const FilterPlan& f) {
@@ -794,7 +877,7 @@ hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st, const Filte
     if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != a.d + 16 || a.ld_q != a.d + 16 || !a.tstat || !a.qstat)
         return hipErrorInvalidValue;
     void* args[] = {const_cast<GemmFilterArgs*>(&a)};
-    const dim3 grid((unsigned)(a.n_qtiles * a.nseg));
+    const dim3 grid((unsigned)(a.g2 < 0 ? (int64_t)a.n_qtiles * a.nseg : (int64_t)a.p1_blocks + a.g2));
     hipError_t e = hipLaunchKernel(fused_ptr(a.d, f), grid, dim3(64 * f.nw), args, f.lds, st);
     if (e != hipSuccess) return e;
     KNN_LAUNCH_CHECK();

@@ -51,6 +51,9 @@ struct GemmFilterArgs {
     int32_t* cand_idx; float* cand_L; float* cand_U; int cap; int cap_seg;
     const float4* tstat;  // fused filter, per 64-row tile: {max tn, max |t - rt|, max |rt|, 0}
     const float2* qstat;  // fused filter, per query: {|q|, |q - rq|} upper bounds (rq: the operand / -2)
+    // fused filter schedule (knn_fused_schedule): p1_blocks whole query tiles, then g2 blocks
+    // over the remaining w2 (query tile, 64-row unit) pairs; tiles64 units per query tile
+    int p1_blocks; int g2; int64_t w2; int64_t tiles64;
     const int32_t* status;  // the call's status word: a set GEMM_UNSAFE bit skips the filter
     const int32_t* gate;    // optional: the filter runs only when *gate != 0 (AUTO's re-run)
 };
@@ -155,6 +158,10 @@ hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st);
 bool knn_fused_supported(int d);
 FilterPlan knn_fused_plan(int d, int k, const FilterStudy* fs = nullptr);  // nw == 0: k too large
 hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu, const FilterStudy* fs = nullptr);
+// fills a.p1_blocks / g2 / w2 / tiles64 for the balanced schedule over `slots` resident
+// blocks; returns the grid, *nseg = the most pieces one query tile gets.  (a.g2 = -1 and
+// a.seg_len / nseg instead: the segment schedule, n_qtiles * nseg blocks.)
+int knn_fused_schedule(GemmFilterArgs& a, int slots, int* nseg);
 hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st, const FilterStudy* fs = nullptr);
 // x [n][ld] (fp32 or bf16) -> bf16 [n][d + 16]: rn(scale * x) | split of norms[r] (or 1 1 1) | 0
 hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int ld, int d, const float* norms, float scale,

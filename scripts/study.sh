@@ -13,7 +13,9 @@ for spec in "${SPECS[@]}"; do
   read -ra W <<< "$spec"
   [ ${#W[@]} -lt 2 ] && continue
   tag=${W[0]}; cfg=${W[1]}
-  env "${W[@]:2}" timeout -k 10 300 python -u bench.py --config $cfg --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-host-path > gpurun_out/${P}_$tag.log 2>&1 || { echo "bench $tag failed"; tail -5 gpurun_out/${P}_$tag.log; exit 1; }
+  EV=(); AR=()
+  for w in "${W[@]:2}"; do if [[ $w == --* ]]; then AR+=("$w"); else EV+=("$w"); fi; done
+  env "${EV[@]}" timeout -k 10 300 python -u bench.py --config $cfg --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-host-path "${AR[@]}" > gpurun_out/${P}_$tag.log 2>&1 || { echo "bench $tag failed"; tail -5 gpurun_out/${P}_$tag.log; exit 1; }
   summ gpurun_out/${P}_$tag.log
 done
 if [ -n "$PYTEST_ENV" ]; then
