@@ -58,7 +58,7 @@ struct knn_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // device workspace
-    DBuf tnorm, tnp, qnorm, gthr, cnt, cand_idx, cand_L, cand_U, fb_list, ctrl, timing;
+    DBuf tnorm, tnp, qnorm, gthr, cnt, cand, fb_list, ctrl, timing;
     DBuf split_t, split_q;  // KNN_ALGO_GEMM_SPLIT / _BF16: bf16 [hi | lo] / rn copies of fp32 rows
     DBuf seg_rec;           // k_direct_tile segment records [nseg][nq][3][k]
     DBuf tmax;              // fused filter: per-64-row train stats {max tn, max |t - rt|, max |rt|, 0}
@@ -390,9 +390,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     HIP_OR_FAIL(c, c->qnorm.ensure(sizeof(float) * nq));
     HIP_OR_FAIL(c, c->gthr.ensure(sizeof(uint32_t) * nq));
     HIP_OR_FAIL(c, c->cnt.ensure(sizeof(int32_t) * nq * 16));  // [2 * nseg][nq], nseg <= 8
-    HIP_OR_FAIL(c, c->cand_idx.ensure(sizeof(int32_t) * nq * cap));
-    HIP_OR_FAIL(c, c->cand_L.ensure(sizeof(float) * nq * cap));
-    HIP_OR_FAIL(c, c->cand_U.ensure(sizeof(float) * nq * cap));
+    HIP_OR_FAIL(c, c->cand.ensure(sizeof(CandRec) * nq * cap));
     HIP_OR_FAIL(c, c->fb_list.ensure(sizeof(int32_t) * nq));
 
     // bf16 MFMA operands (rounded fp32 rows or bf16 data) run the fused-norm filter
@@ -502,8 +500,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     g.k = k; g.seg_len = seg_len; g.nseg = nseg;
     g.coef = coef; g.eta = eta;
     g.gthr = c->gthr.as<uint32_t>();
-    g.cnt = c->cnt.as<int32_t>(); g.cand_idx = c->cand_idx.as<int32_t>();
-    g.cand_L = c->cand_L.as<float>(); g.cand_U = c->cand_U.as<float>(); g.cap = cap; g.cap_seg = cap / nseg;
+    g.cnt = c->cnt.as<int32_t>(); g.cand = c->cand.as<CandRec>(); g.cap = cap; g.cap_seg = cap / nseg;
     g.tstat = fused ? c->tmax.as<float4>() : nullptr;
     g.qstat = fused ? c->qstat.as<float2>() : nullptr;
     g.status = c->ctrl.as<int32_t>();
@@ -535,7 +532,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     RescoreArgs r{};
     r.train = tr->feat; r.labels = tr->labels; r.ld_t = tr->ld;
     r.test = te->feat; r.ld_q = te->ld; r.nq = nq; r.d = d; r.k = k; r.C = C; r.elem = dtype;
-    r.cnt = g.cnt; r.cand_idx = g.cand_idx; r.cand_L = g.cand_L; r.cand_U = g.cand_U; r.cap = cap;
+    r.cnt = g.cnt; r.cand = g.cand; r.cap = cap;
     r.nseg = 2 * nseg; r.cap_seg = g.cap_seg / 2;  // sub-slices: (segment, lane half)
     r.out = out; r.status = c->ctrl.as<int32_t>();
     r.fb_list = c->fb_list.as<int32_t>(); r.fb_count = c->ctrl.as<int32_t>() + 1;
@@ -633,7 +630,7 @@ knn_status knn_create(knn_ctx** out, const knn_opts* opts) {
 void knn_destroy(knn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    for (DBuf* b : {&c->tnorm, &c->tnp, &c->qnorm, &c->gthr, &c->cnt, &c->cand_idx, &c->cand_L, &c->cand_U,
+    for (DBuf* b : {&c->tnorm, &c->tnp, &c->qnorm, &c->gthr, &c->cnt, &c->cand,
                     &c->fb_list, &c->ctrl, &c->timing, &c->split_t, &c->split_q, &c->seg_rec, &c->tmax, &c->qstat, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
                     &c->h_dist, &c->h_idx})
         b->release();

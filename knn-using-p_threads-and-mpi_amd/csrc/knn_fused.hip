@@ -134,11 +134,13 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     constexpr int VPS = (16 + NS - 1) / NS;      // fast-test values per k-step per accumulator
     constexpr int NR = NBUF + 1;                 // norm ring slots: tiles it-1 .. it+NBUF-1
     constexpr int RS = BN;                       // ring slot: BN row norms
-    static_assert(NBUF == 2 || NBUF == 3 || NBUF == 4, "tile buffers");
-    // NBUF = 4: tiles go in pairs -- one barrier per two tiles; the DMA of tile it + 2 is
-    // issued during step it into the buffer tile it - 2 used (read before this pair's barrier)
-    constexpr bool PAIR = NBUF == 4;
-    constexpr int AHEAD = PAIR ? 2 : NBUF - 1;  // tiles between a step and the tile it DMAs
+    static_assert(NBUF == 2 || NBUF == 3 || NBUF == 4 || NBUF == 6, "tile buffers");
+    // NBUF = 2 GRP (4, 6): tiles go in groups of GRP -- one barrier per group; the DMA of tile
+    // it + GRP is issued during step it into the buffer tile it - GRP used (read before this
+    // group's barrier)
+    constexpr int GRP = (NBUF == 4 || NBUF == 6) ? NBUF / 2 : 1;
+    constexpr bool PAIR = GRP > 1;
+    constexpr int AHEAD = PAIR ? GRP : NBUF - 1;  // tiles between a step and the tile it DMAs
     static_assert(RG == 1 || RG == 2, "row groups");
     static_assert(KR == 0 || KR == 16 || KR == 32, "register lists: k <= 16, k <= 32, or LDS heaps");
     constexpr bool RL = KR > 0;       // thresholds from per-lane register lists (else LDS heaps)
@@ -344,9 +346,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     auto store_cand = [&](float L, float U, int64_t t) __attribute__((always_inline)) {
         if (ccnt < cap_sub) {
             const int64_t o = q * (int64_t)a.cap + (int64_t)(2 * seg + h) * cap_sub + ccnt;
-            a.cand_idx[o] = (int32_t)t;
-            a.cand_L[o] = L;
-            a.cand_U[o] = U;
+            a.cand[o] = CandRec{(int32_t)t, L, U};
         }
         ccnt++;
     };
@@ -598,7 +598,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // per-64-row maximum train norm of the tile in the pipeline (tile it) and of tile it-1
     const int64_t tile0 = row_begin >> 6;
     float2 tm_prev = make_float2(0.0f, 0.0f);
-    float2 tm_odd = make_float2(0.0f, 0.0f);  // PAIR: the second tile's term, loaded with the first's
+    float2 tmg[GRP];  // PAIR: the group's tile terms, loaded after its barrier
     auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
         if ((it & 63) == 63) {
             if (a.nseg > 1 && qvalid) {
@@ -617,7 +617,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         if constexpr (PAIR) {
             // pair (it, it + 1) starts: both tiles have landed (every wave's pieces), and
             // every wave is done with the previous pair's buffers
-            if ((it & 1) == 0) wait_dma_barrier(0);
+            if (it % GRP == 0) wait_dma_barrier(0);
         } else {
             const bool keep_next = NBUF == 3 && it + 1 < ntiles && (LATE_DMA || !dirty);
             wait_dma_barrier(keep_next ? n_dma_wave : 0);
@@ -629,12 +629,14 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         if constexpr (PAIR) {
             // both tiles' maxima after the pair's barrier: no compiler wait on a load issued
             // before the DMA of the second step (it would wait for that DMA too)
-            if ((it & 1) == 0) {
-                tm_cur = tile_q(tile0 + ((it * BN) >> 6));
-                tm_odd = tile_q(tile0 + ((min(it + 1, ntiles - 1) * BN) >> 6));
-            } else {
-                tm_cur = tm_odd;
+            const int gi = it % GRP;
+            if (gi == 0) {
+#pragma unroll
+                for (int g = 0; g < GRP; g++) tmg[g] = tile_q(tile0 + ((min(it + g, ntiles - 1) * BN) >> 6));
             }
+            tm_cur = tmg[0];
+#pragma unroll
+            for (int g = 1; g < GRP; g++) tm_cur = gi == g ? tmg[g] : tm_cur;
         } else {
             tm_cur = tile_q(tile0 + ((it * BN) >> 6));
         }
@@ -646,10 +648,10 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
 #endif
         const DmaTile dd = dma_desc((it + AHEAD) % NBUF, (it + AHEAD) % NR, row_begin + (int64_t)(it + AHEAD) * BN);
         const float tf = it > 0 ? tf_of(tm_prev) : -INF;
-        const uint32_t uY = step(X, Y, it % NBUF, dma_on && !LATE_DMA, dd, tf, PAIR && (it & 1));
-        // PAIR: the odd tile is resident since this pair's barrier -- its first fragments
+        const uint32_t uY = step(X, Y, it % NBUF, dma_on && !LATE_DMA, dd, tf, PAIR && it % GRP != 0);
+        // PAIR: the group's next tile is resident since its barrier -- its first fragments
         // are read now, so their latency hides under the slow path below
-        if (PAIR && (it & 1) == 0 && it + 1 < ntiles) prefetch((it + 1) % NBUF);
+        if (PAIR && it % GRP != GRP - 1 && it + 1 < ntiles) prefetch((it + 1) % NBUF);
         KNN_TSTAMP(t2);
 #ifndef KNN_ABLATE_NO_SLOW
         if (uY) {
@@ -826,7 +828,8 @@ FilterPlan knn_fused_plan(int d, int k, const FilterStudy* fs) {
         return f;
     };
     const bool force8 = fs && fs->shape[0] == 'w' && fs->shape[1] == '8';
-    const int nb = fs && (fs->nbuf == 3 || fs->nbuf == 4) ? fs->nbuf : 2;  // kernel study: 3 buffers, or pairs (4)
+    // study: 3 buffers or pairs (4); triples (6) measured slower (A 28.0 -> 31.9 ms, B 749 -> 995)
+    const int nb = fs && (fs->nbuf == 3 || fs->nbuf == 4) ? fs->nbuf : 2;
     const bool force4 = fs && fs->shape[0] == 'w' && fs->shape[1] == '4';
     // d = 64 with register lists: 8-wave blocks in pairs like d >= 128 (B, same box: 765 ms
     // with 4-wave blocks in pairs, 743 with 8-wave) -- 256 queries share each tile's DMA

@@ -38,6 +38,10 @@ struct ExactScanArgs {
     int q_lds_bytes;                              // set by the launcher
 };
 
+// one kept candidate of the GEMM filters: its train row and certified bounds L <= D <= U
+// (one 12-byte store per kept row)
+struct CandRec { int32_t idx; float L; float U; };
+
 struct GemmFilterArgs {
     const void* train; int64_t nt; int ld_t;      // ld in elements
     const void* test; int64_t nq; int ld_q; int d;
@@ -48,7 +52,7 @@ struct GemmFilterArgs {
     uint32_t* gthr;
     unsigned long long* timing;  // KNN_FILTER_TIMING builds: per-phase shader clocks (else NULL)
     int32_t* cnt;  // [nseg][nq] kept rows per (segment, query)
-    int32_t* cand_idx; float* cand_L; float* cand_U; int cap; int cap_seg;
+    CandRec* cand; int cap; int cap_seg;  // [nq][cap] candidate records
     const float4* tstat;  // fused filter, per 64-row tile: {max tn, max |t - rt|, max |rt|, 0}
     const float2* qstat;  // fused filter, per query: {|q|, |q - rq|} upper bounds (rq: the operand / -2)
     // fused filter schedule (knn_fused_schedule): p1_blocks whole query tiles, then g2 blocks
@@ -61,7 +65,7 @@ struct GemmFilterArgs {
 struct RescoreArgs {
     const void* train; const int32_t* labels; int ld_t;
     const void* test; int ld_q; int64_t nq; int d; int k; int C; int elem;
-    const int32_t* cnt; const int32_t* cand_idx; const float* cand_L; const float* cand_U; int cap;
+    const int32_t* cnt; const CandRec* cand; int cap;
     int nseg; int cap_seg;
     QueryOut out; int32_t* status;
     int32_t* fb_list; int32_t* fb_count;

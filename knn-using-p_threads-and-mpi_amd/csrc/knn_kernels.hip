@@ -886,9 +886,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
         if (slot < cap_sub) {
             const int64_t qq = g1 ? q[QG - 1] : q[0];
             const int64_t o = qq * (int64_t)a.cap + (int64_t)(2 * seg + h) * cap_sub + slot;
-            a.cand_idx[o] = (int32_t)t;
-            a.cand_L[o] = L;
-            a.cand_U[o] = U;
+            a.cand[o] = CandRec{(int32_t)t, L, U};
         }
         slot++;
         float& rt = g1 ? root[QG - 1] : root[0];
@@ -1253,7 +1251,7 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
         const int e = lane + 64 * i;
         const int64_t o = position(e);
         if (e < total) {
-            const uint32_t u = f2o(a.cand_U[o]);
+            const uint32_t u = f2o(a.cand[o].U);
             if (e < su_cap) su[e] = u;
             umin = min(umin, u);
             umax = max(umax, u);
@@ -1278,7 +1276,7 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
             // position() shuffles across the wave: every lane calls it (wave-uniform branch)
             const int64_t o = 64 * i + 63 >= su_cap ? position(e) : 0;
             uint32_t u = 0xffffffffu;
-            if (e < total) u = e < su_cap ? su[e] : f2o(a.cand_U[o]);
+            if (e < total) u = e < su_cap ? su[e] : f2o(a.cand[o].U);
             c += __popcll(__ballot(e < total && u <= mid));
         }
         if (c >= k) hi = mid; else lo = mid + 1;
@@ -1290,8 +1288,8 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
     for (int i = 0; i < nreg; i++) {
         const int e = lane + 64 * i;
         const int64_t o = position(e);
-        const bool sv = e < total && a.cand_L[o] <= thr;
-        const int32_t t = sv ? a.cand_idx[o] : 0;
+        const bool sv = e < total && a.cand[o].L <= thr;
+        const int32_t t = sv ? a.cand[o].idx : 0;
         const u64 bal = __ballot(sv);
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
