@@ -203,8 +203,17 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         qe2 = 2.0f * qs.x * (1.0f + 0x1p-17f);
         eq2 = 2.0f * qs.y * (1.0f + 0x1p-17f);
     }
+    // the tile's stats by a scalar load (constant address space, wave-uniform index): counted
+    // by lgkmcnt, so using them never waits on the vector-memory count the tile DMAs share
     auto tile_q = [&](int64_t tile) __attribute__((always_inline)) -> float2 {
-        const float4 t = a.tstat[tile];
+        const int ti = __builtin_amdgcn_readfirstlane((int)tile);
+#ifdef __HIP_DEVICE_COMPILE__
+        typedef __attribute__((address_space(4))) const float* cfloatp;
+        const cfloatp p = (cfloatp)(a.tstat + ti);
+        const float4 t = make_float4(p[0], p[1], p[2], p[3]);
+#else
+        const float4 t = a.tstat[ti];  // (the host pass only parses device code)
+#endif
         return make_float2(t.x, fmaf(qe2, t.y, eq2 * t.z));
     };
 
