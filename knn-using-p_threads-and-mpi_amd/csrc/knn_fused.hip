@@ -334,11 +334,10 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             __builtin_amdgcn_sched_barrier(0);  // keep this k-step's order (prefetch, MFMA, VALU)
         }
         if constexpr (!PSTEP) {
-            // only whether some value passes; the slow path builds the set itself (pass_set)
-            float m = mn[0];
+            // which accumulators hold a passing value; the slow path builds their value sets
+            // (pass_set) -- usually one of the two
 #pragma unroll
-            for (int c = 1; c < NACC; c++) m = fminf(m, mn[c]);
-            u = __ballot(m <= tf) != 0ull ? 0xffffffffu : 0u;
+            for (int c = 0; c < NACC; c++) u |= __ballot(mn[c] <= tf) != 0ull ? (0xffffu << (16 * c)) : 0u;
         }
         return u;
     };
@@ -426,19 +425,21 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // then scalar ops (the !PSTEP variant builds it only on tiles some value passes).
     // Measured (same box): sets by groups of 4 values (a min of 4 per ballot) are slower on A
     // and B -- the extra slow-path visits cost more than the scalar ops they save.
-    auto pass_set = [&](floatx16 (&Y)[NACC], float tf) __attribute__((always_inline)) -> uint32_t {
+    auto pass_set = [&](floatx16 (&Y)[NACC], float tf, uint32_t acc = 0xffffffffu) __attribute__((always_inline)) -> uint32_t {
         uint32_t u = 0u;
 #pragma unroll
         for (int c = 0; c < NACC; c++)
+            if ((acc >> (16 * c)) & 1u) {  // (wave-uniform) only the accumulators that pass
 #pragma unroll
-            for (int r = 0; r < 16; r++) u |= (__ballot(Y[c][r] <= tf) != 0ull ? 1u : 0u) << (16 * c + r);
+                for (int r = 0; r < 16; r++) u |= (__ballot(Y[c][r] <= tf) != 0ull ? 1u : 0u) << (16 * c + r);
+            }
         return u;
     };
     // immediate slow path: the passing values of tile tp, visited by index; the two lanes
     // of a query take turns (one heap writer at a time)
     auto slow = [&](floatx16 (&Y)[NACC], int tp, float tf, float2 tq, uint32_t u) {
         const int64_t tbase = row_begin + (int64_t)tp * BN;
-        if constexpr (!PSTEP) u = pass_set(Y, tf);
+        if constexpr (!PSTEP) u = pass_set(Y, tf, u);
         while (u) {
             const int v = __builtin_ctz(u);
             u &= u - 1u;
@@ -493,7 +494,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     auto slow_rl = [&](floatx16 (&Y)[NACC], int tp, float tf, float2 tq, uint32_t u) {
         if constexpr (RL) {
             const int64_t tbase = row_begin + (int64_t)tp * BN;
-            if constexpr (!PSTEP) u = pass_set(Y, tf);
+            if constexpr (!PSTEP) u = pass_set(Y, tf, u);
             while (u) {
                 const int v = __builtin_ctz(u);
                 u &= u - 1u;
@@ -561,7 +562,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     };
     auto record = [&](floatx16 (&Y)[NACC], int tp, float tf, float2 tq, uint32_t u) {
         const int64_t tbase = row_begin + (int64_t)tp * BN;
-        if constexpr (!PSTEP) u = pass_set(Y, tf);
+        if constexpr (!PSTEP) u = pass_set(Y, tf, u);
 #ifdef KNN_FILTER_TIMING
         tph[4] += 1;
         tph[5] += __builtin_popcount(u);
@@ -657,6 +658,8 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
 #endif
         const DmaTile dd = dma_desc((it + AHEAD) % NBUF, (it + AHEAD) % NR, row_begin + (int64_t)(it + AHEAD) * BN);
         const float tf = it > 0 ? tf_of(tm_prev) : -INF;
+        // (measured slower: both tiles of the next pair DMA'd in one burst after the even step,
+        // A 28.0 -> 28.5 ms, B 752 -> 802 ms)
         const uint32_t uY = step(X, Y, it % NBUF, dma_on && !LATE_DMA, dd, tf, PAIR && it % GRP != 0);
         // PAIR: the group's next tile is resident since its barrier -- its first fragments
         // are read now, so their latency hides under the slow path below
@@ -696,8 +699,9 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         const int last = ntiles - 1;
         auto drain = [&](floatx16 (&Lc)[NACC]) {
             const float tf = tf_of(tm_prev);
-            const uint32_t u = pass_set(Lc, tf);
+            uint32_t u = pass_set(Lc, tf);
             if (u) {
+                if constexpr (!PSTEP) u = 0xffffffffu;  // the slow paths rebuild the set per accumulator
                 if constexpr (RL) slow_rl(Lc, last, tf, tm_prev, u);
                 else if constexpr (DEFER) record(Lc, last, tf, tm_prev, u);
                 else slow(Lc, last, tf, tm_prev, u);
