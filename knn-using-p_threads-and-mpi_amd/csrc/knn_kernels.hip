@@ -453,27 +453,49 @@ __global__ __launch_bounds__(256) void k_row_norms(const E* __restrict__ x, int6
                                                    float2* __restrict__ qstat, float oscale) {
     if (gate && *gate == 0) return;  // a gated stage (AUTO's re-run) that is not taken
     // rows [n, n + 64) of out/outp get +inf: the GEMM filter's tile tail reads them
-    int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    float s = 0.0f, se = 0.0f, sr = 0.0f;
+    const int lane = threadIdx.x & 63;
+    const int64_t r0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63);  // the wave's 64 rows
+    const int64_t r = r0 + lane;
     const bool rstat = tstat || qstat;
     const float inv = 1.0f / oscale;  // 1 or -0.5: exact
-    auto acc = [&](float v) __attribute__((always_inline)) {
-        s = fmaf(v, v, s);
-        if (rstat) {
-            const float rv = __uint_as_float(bf16_rne(oscale * v) << 16) * inv;
-            const float e = v - rv;
-            se = fmaf(e, e, se);
-            sr = fmaf(rv, rv, sr);
+    // 16 lanes per row, 4 rows at a time (coalesced 256-byte reads); lane r0 + l ends with
+    // row l's sums.  The fp32 sum order differs from a serial chain: the certificate's bound
+    // on a norm (d u relative) holds for any order.
+    float s = 0.0f, se = 0.0f, sr = 0.0f;
+    const int g = lane >> 4, l16 = lane & 15;
+    for (int r4 = 0; r4 < 16; r4++) {
+        const int64_t row = r0 + 4 * r4 + g;
+        float a = 0.0f, ae = 0.0f, ar = 0.0f;
+        auto acc = [&](float v) __attribute__((always_inline)) {
+            a = fmaf(v, v, a);
+            if (rstat) {
+                const float rv = __uint_as_float(bf16_rne(oscale * v) << 16) * inv;
+                const float e = v - rv;
+                ae = fmaf(e, e, ae);
+                ar = fmaf(rv, rv, ar);
+            }
+        };
+        if (row < n) {
+            const E* xr = x + row * ld;
+            int i = 4 * l16;
+            for (; i + 4 <= d; i += 64) {
+                const float4 v = load4(xr + i);
+                acc(v.x); acc(v.y); acc(v.z); acc(v.w);
+            }
+            for (int t = (d & ~3) + l16; t < d; t += 16) acc(widen(xr[t]));  // the d % 4 tail
         }
-    };
+#pragma unroll
+        for (int j = 8; j > 0; j >>= 1) {
+            a += __shfl_xor(a, j);
+            if (rstat) { ae += __shfl_xor(ae, j); ar += __shfl_xor(ar, j); }
+        }
+        // lane l takes row l = 4 r4 + (l & 3) from lane 16 (l & 3) of this round
+        const float va = __shfl(a, 16 * (lane & 3));
+        const float vae = rstat ? __shfl(ae, 16 * (lane & 3)) : 0.0f;
+        const float var = rstat ? __shfl(ar, 16 * (lane & 3)) : 0.0f;
+        if ((lane >> 2) == r4) { s = va; se = vae; sr = var; }
+    }
     if (r < n) {
-        const E* row = x + r * ld;
-        int i = 0;
-        for (; i + 4 <= d; i += 4) {
-            const float4 v = load4(row + i);
-            acc(v.x); acc(v.y); acc(v.z); acc(v.w);
-        }
-        for (; i < d; i++) acc(widen(row[i]));
         out[r] = s;
         if (qstat) qstat[r] = make_float2(norm_ub(s, d), norm_ub(se, d));
         if (outp) outp[r] = c1 * s;
