@@ -36,6 +36,12 @@
 #ifndef KNN_FUSED_PRIO
 #define KNN_FUSED_PRIO 0  // 1 (study): s_setprio 1 for the second half of the waves
 #endif
+#ifndef KNN_FUSED_SB_MASK
+#define KNN_FUSED_SB_MASK 0  // instruction types the per-k-step scheduling barrier lets through
+#endif
+#ifndef KNN_FUSED_SB_STEPS
+#define KNN_FUSED_SB_STEPS 64  // k-steps closed by a scheduling barrier (the first ones)
+#endif
 #ifndef KNN_FUSED_ROW_NORM
 #define KNN_FUSED_ROW_NORM 0  // 1: the slow path's bounds use each row's norm (an LDS ring filled by DMA)
 #endif
@@ -331,7 +337,10 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                 }
 #endif
             }
-            __builtin_amdgcn_sched_barrier(0);  // keep this k-step's order (prefetch, MFMA, VALU)
+#ifndef KNN_FUSED_NO_SCHED_BARRIER
+            if (s < KNN_FUSED_SB_STEPS)
+                __builtin_amdgcn_sched_barrier(KNN_FUSED_SB_MASK);  // keep this k-step's order (prefetch, MFMA, VALU)
+#endif
         }
         if constexpr (!PSTEP) {
             // which accumulators hold a passing value; the slow path builds their value sets
