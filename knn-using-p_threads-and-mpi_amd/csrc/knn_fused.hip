@@ -39,6 +39,9 @@
 #ifndef KNN_FUSED_SB_MASK
 #define KNN_FUSED_SB_MASK 0  // instruction types the per-k-step scheduling barrier lets through
 #endif
+#ifndef KNN_FUSED_RELAX
+#define KNN_FUSED_RELAX 0  // 1 (study): no per-k-step barrier; wait states before reading accumulators
+#endif
 #ifndef KNN_FUSED_SB_STEPS
 #define KNN_FUSED_SB_STEPS 64  // k-steps closed by a scheduling barrier (the first ones)
 #endif
@@ -298,6 +301,13 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         const unsigned char* tile = tiles + buf * TILE;
         const unsigned char* a0p = tile + j * STRIDE + 16 * h;
         const unsigned char* a1p = tile + ((RG == 2 ? 32 : 0) + j) * STRIDE + 16 * h;
+        if constexpr (KNN_FUSED_RELAX) {
+            // the accumulators Y were written by the previous step's last MFMAs: wait states
+            // before any VALU of this (freely scheduled) step reads them
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7");
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int c = 0; c < NACC; c++) X[c] = floatx16{};
         uint32_t u = 0u;
@@ -337,7 +347,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                 }
 #endif
             }
-#ifndef KNN_FUSED_NO_SCHED_BARRIER
+#if !defined(KNN_FUSED_NO_SCHED_BARRIER) && !KNN_FUSED_RELAX
             if (s < KNN_FUSED_SB_STEPS)
                 __builtin_amdgcn_sched_barrier(KNN_FUSED_SB_MASK);  // keep this k-step's order (prefetch, MFMA, VALU)
 #endif
@@ -707,6 +717,11 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         // drain: the last tile's accumulators are in accA (ntiles odd) or accB (even)
         const int last = ntiles - 1;
         auto drain = [&](floatx16 (&Lc)[NACC]) {
+            if constexpr (KNN_FUSED_RELAX) {
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7");
+                __builtin_amdgcn_sched_barrier(0);
+            }
             const float tf = tf_of(tm_prev);
             uint32_t u = pass_set(Lc, tf);
             if (u) {
