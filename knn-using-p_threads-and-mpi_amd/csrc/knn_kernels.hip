@@ -130,10 +130,12 @@ __device__ __forceinline__ u64 vote_ballot(const int (&lab)[R], int k) {
 // idx, label) and, when o.pred is set, the vote of main.cpp:64-78.
 // counts: wave-private LDS array of C ints, or NULL for the table-free vote_ballot
 // (class counts above KNN_VOTE_LDS_MAX_C).  Runs on one wave.
+// lab0 (optional): the label of element `lane` of T[0], already loaded by the caller.
 // ---------------------------------------------------------------------------------
 template <int R>
 __device__ void finish_query(const u64 (&T)[R], int k, int C, const int32_t* __restrict__ labels,
-                             int* counts, int64_t q, const QueryOut& o, int32_t* __restrict__ status) {
+                             int* counts, int64_t q, const QueryOut& o, int32_t* __restrict__ status,
+                             const int* lab0 = nullptr) {
     const int lane = lane_id();
     const bool vote = o.pred != nullptr;
     const bool lds_vote = vote && counts != nullptr;
@@ -154,7 +156,7 @@ __device__ void finish_query(const u64 (&T)[R], int k, int C, const int32_t* __r
             const int64_t off = q * o.stride + e;
             if (key != KEY_NONE) {
                 int32_t idx = (int32_t)(uint32_t)(key & 0xffffffffull);
-                int lab = labels[idx];
+                const int lab = (r == 0 && lab0) ? *lab0 : labels[idx];
                 if (o.dist) o.dist[off] = __uint_as_float((uint32_t)(key >> 32));
                 if (o.idx) o.idx[off] = (int32_t)(o.idx_base + idx);
                 if (o.label) o.label[off] = lab;
@@ -1352,6 +1354,9 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
         // ties); an infinite distance gets the key ~0 << 32 | idx (after every finite key,
         // distinct) and reads KEY_NONE again after the permute.
         const uint32_t t = lane < m ? su[lane] : 0u;
+        // the survivor's label now: its load lands under the distance's row loads (no
+        // dependent label read after the selection)
+        const int lab = lane < m ? a.labels[t] : -1;
         u64 key = KEY_NONE;
         if (lane < m) {
             key = make_key(direct_dist_batched(qs, train + (int64_t)t * a.ld_t, a.d), t);
@@ -1367,6 +1372,9 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
         const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)key);
         const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)(key >> 32));
         T[0] = hi == 0xffffffffu ? KEY_NONE : (((u64)hi << 32) | lo);
+        const int labp = __builtin_amdgcn_ds_permute(dst, lab);
+        finish_query<R>(T, k, a.C, a.labels, counts, q, a.out, a.status, &labp);
+        return;
     } else {
         u64 kth = KEY_NONE;
         for (int b = 0; b < m; b += 64) {
