@@ -39,6 +39,9 @@
 #ifndef KNN_FUSED_SB_MASK
 #define KNN_FUSED_SB_MASK 0  // instruction types the per-k-step scheduling barrier lets through
 #endif
+#ifndef KNN_FUSED_GROUP_SET
+#define KNN_FUSED_GROUP_SET 1  // the lazy pass set by groups of 4 values first (B 703 -> 674 ms, A same)
+#endif
 #ifndef KNN_FUSED_RELAX
 #define KNN_FUSED_RELAX 0  // 1 (study): no per-k-step barrier; wait states before reading accumulators
 #endif
@@ -449,8 +452,22 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
 #pragma unroll
         for (int c = 0; c < NACC; c++)
             if ((acc >> (16 * c)) & 1u) {  // (wave-uniform) only the accumulators that pass
+#if KNN_FUSED_GROUP_SET
+                // then only the groups of 4 values (rows 8g .. 8g+3 of the lane half) whose
+                // minimum passes
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const float gm = fminf(fminf(Y[c][4 * g], Y[c][4 * g + 1]), fminf(Y[c][4 * g + 2], Y[c][4 * g + 3]));
+                    if (__ballot(gm <= tf)) {
+#pragma unroll
+                        for (int r = 4 * g; r < 4 * g + 4; r++)
+                            u |= (__ballot(Y[c][r] <= tf) != 0ull ? 1u : 0u) << (16 * c + r);
+                    }
+                }
+#else
 #pragma unroll
                 for (int r = 0; r < 16; r++) u |= (__ballot(Y[c][r] <= tf) != 0ull ? 1u : 0u) << (16 * c + r);
+#endif
             }
         return u;
     };
