@@ -36,17 +36,8 @@
 #ifndef KNN_FUSED_PRIO
 #define KNN_FUSED_PRIO 0  // 1 (study): s_setprio 1 for the second half of the waves
 #endif
-#ifndef KNN_FUSED_SB_MASK
-#define KNN_FUSED_SB_MASK 0  // instruction types the per-k-step scheduling barrier lets through
-#endif
 #ifndef KNN_FUSED_GROUP_SET
 #define KNN_FUSED_GROUP_SET 1  // the lazy pass set by groups of 4 values first (B 703 -> 674 ms, A same)
-#endif
-#ifndef KNN_FUSED_RELAX
-#define KNN_FUSED_RELAX 0  // 1 (study): no per-k-step barrier; wait states before reading accumulators
-#endif
-#ifndef KNN_FUSED_SB_STEPS
-#define KNN_FUSED_SB_STEPS 64  // k-steps closed by a scheduling barrier (the first ones)
 #endif
 #ifndef KNN_FUSED_ROW_NORM
 #define KNN_FUSED_ROW_NORM 0  // 1: the slow path's bounds use each row's norm (an LDS ring filled by DMA)
@@ -304,13 +295,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         const unsigned char* tile = tiles + buf * TILE;
         const unsigned char* a0p = tile + j * STRIDE + 16 * h;
         const unsigned char* a1p = tile + ((RG == 2 ? 32 : 0) + j) * STRIDE + 16 * h;
-        if constexpr (KNN_FUSED_RELAX) {
-            // the accumulators Y were written by the previous step's last MFMAs: wait states
-            // before any VALU of this (freely scheduled) step reads them
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7");
-            __builtin_amdgcn_sched_barrier(0);
-        }
+        KNN_STUDY_STEP_HEAD();
 #pragma unroll
         for (int c = 0; c < NACC; c++) X[c] = floatx16{};
         uint32_t u = 0u;
@@ -350,10 +335,9 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                 }
 #endif
             }
-#if !defined(KNN_FUSED_NO_SCHED_BARRIER) && !KNN_FUSED_RELAX
-            if (s < KNN_FUSED_SB_STEPS)
-                __builtin_amdgcn_sched_barrier(KNN_FUSED_SB_MASK);  // keep this k-step's order (prefetch, MFMA, VALU)
-#endif
+            // keep this k-step's order (prefetch, MFMA, VALU): load-bearing -- relaxed, the
+            // filter runs 11 % faster and drops true neighbours (DESIGN.md "Next" 1)
+            KNN_STUDY_KSTEP_BARRIER(s);
         }
         if constexpr (!PSTEP) {
             // which accumulators hold a passing value; the slow path builds their value sets
@@ -734,11 +718,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         // drain: the last tile's accumulators are in accA (ntiles odd) or accB (even)
         const int last = ntiles - 1;
         auto drain = [&](floatx16 (&Lc)[NACC]) {
-            if constexpr (KNN_FUSED_RELAX) {
-                __builtin_amdgcn_sched_barrier(0);
-                asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7");
-                __builtin_amdgcn_sched_barrier(0);
-            }
+            KNN_STUDY_STEP_HEAD();
             const float tf = tf_of(tm_prev);
             uint32_t u = pass_set(Lc, tf);
             if (u) {
