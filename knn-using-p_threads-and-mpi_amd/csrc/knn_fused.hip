@@ -36,6 +36,9 @@
 #ifndef KNN_FUSED_PRIO
 #define KNN_FUSED_PRIO 0  // 1 (study): s_setprio 1 for the second half of the waves
 #endif
+#ifndef KNN_FUSED_SHARE_EVERY
+#define KNN_FUSED_SHARE_EVERY 64  // tiles between threshold exchanges of a query's pieces (gthr)
+#endif
 #ifndef KNN_FUSED_GROUP_SET
 #define KNN_FUSED_GROUP_SET 1  // the lazy pass set by groups of 4 values first (B 703 -> 674 ms, A same)
 #endif
@@ -630,7 +633,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     float2 tm_prev = make_float2(0.0f, 0.0f);
     float2 tmg[GRP];  // PAIR: the group's tile terms, loaded after its barrier
     auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
-        if ((it & 63) == 63) {
+        if ((it & (KNN_FUSED_SHARE_EVERY - 1)) == KNN_FUSED_SHARE_EVERY - 1) {
             if (a.nseg > 1 && qvalid) {
                 if constexpr (RL) {  // publish this query's bound (the heap path does it per accept)
                     if (h == 0 && thr < published) {
