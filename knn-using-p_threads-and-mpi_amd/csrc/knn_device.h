@@ -137,6 +137,15 @@ __device__ __forceinline__ float u4getf(const uint4& v, int i) {
     return __uint_as_float(i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w);
 }
 
+// Wait states in front of each LDS-DMA issue (after its M0 write): the compiler's hazard
+// checks do not look inside inline asm, and a VALU write of the SGPR base the load reads
+// (v_readfirstlane) needs 5 of them before a vector-memory instruction reads it
+#ifndef KNN_DMA_NOPS
+#define KNN_DMA_NOPS "0"
+#endif
+#ifndef KNN_DMA_TAIL
+#define KNN_DMA_TAIL ""  // study: instructions after each LDS-DMA issue (e.g. "\n\ts_nop 7")
+#endif
 // LDS-DMA issued by inline asm: the compiler does not see these as LDS writes, so it
 // does not put a vmcnt(0) in front of the next LDS read (which would serialise every
 // tile's compute behind the DMA of the tile after it); the kernel orders them itself
@@ -146,7 +155,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 }
 __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds) {
     lds = __builtin_amdgcn_readfirstlane(lds);
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(lds)
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop " KNN_DMA_NOPS "\n\tglobal_load_lds_dwordx4 %0, off" KNN_DMA_TAIL ::"v"(gsrc), "s"(lds)
                  : "memory", "m0");
 }
 // a wave-uniform value the compiler may have kept in VGPRs, as SGPRs
@@ -160,13 +169,13 @@ __device__ __forceinline__ const void* sgpr_ptr(const void* p) {
 __device__ __forceinline__ void dma16s(uint32_t voff, const void* sbase, uint32_t lds) {
     sbase = sgpr_ptr(sbase);
     lds = __builtin_amdgcn_readfirstlane(lds);
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop " KNN_DMA_NOPS "\n\tglobal_load_lds_dwordx4 %0, %1" KNN_DMA_TAIL ::"v"(voff), "s"(sbase), "s"(lds)
                  : "memory", "m0");
 }
 __device__ __forceinline__ void dma4s(uint32_t voff, const void* sbase, uint32_t lds) {
     sbase = sgpr_ptr(sbase);
     lds = __builtin_amdgcn_readfirstlane(lds);
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sbase), "s"(lds)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop " KNN_DMA_NOPS "\n\tglobal_load_lds_dword %0, %1" KNN_DMA_TAIL ::"v"(voff), "s"(sbase), "s"(lds)
                  : "memory", "m0");
 }
 // wait until at most n (wave-uniform, <= 15) vector-memory ops of this wave are in

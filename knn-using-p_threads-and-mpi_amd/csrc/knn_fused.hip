@@ -36,6 +36,9 @@
 #ifndef KNN_FUSED_PRIO
 #define KNN_FUSED_PRIO 0  // 1 (study): s_setprio 1 for the second half of the waves
 #endif
+#ifndef KNN_FUSED_LATE_DMA
+#define KNN_FUSED_LATE_DMA 0
+#endif
 #ifndef KNN_FUSED_SHARE_EVERY
 #define KNN_FUSED_SHARE_EVERY 64  // tiles between threshold exchanges of a query's pieces (gthr)
 #endif
@@ -625,7 +628,8 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
 #ifndef KNN_FUSED_EARLY_DMA
 #define KNN_FUSED_EARLY_DMA 0
 #endif
-    constexpr bool LATE_DMA = NBUF == 3 && !KNN_FUSED_EARLY_DMA;
+    // KNN_FUSED_LATE_DMA (study): tiles in groups also issue their DMA after the step
+    constexpr bool LATE_DMA = (NBUF == 3 && !KNN_FUSED_EARLY_DMA) || (NBUF >= 4 && KNN_FUSED_LATE_DMA);
     constexpr bool DEFER = NW == 8 && KNN_FUSED_DEFER && !RL;
     constexpr int DEFER_EVERY = KNN_FUSED_DEFER_EVERY;
     // per-64-row maximum train norm of the tile in the pipeline (tile it) and of tile it-1
