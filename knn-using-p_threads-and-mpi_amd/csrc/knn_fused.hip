@@ -39,6 +39,9 @@
 #ifndef KNN_FUSED_LATE_DMA
 #define KNN_FUSED_LATE_DMA 0
 #endif
+#ifndef KNN_FUSED_DMA_OFS
+#define KNN_FUSED_DMA_OFS 0  // k-steps the tile's DMA pieces are shifted by within the step (study)
+#endif
 #ifndef KNN_FUSED_SHARE_EVERY
 #define KNN_FUSED_SHARE_EVERY 64  // tiles between threshold exchanges of a query's pieces (gthr)
 #endif
@@ -277,7 +280,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     auto dma_at = [&](int s, bool on, const DmaTile& d) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < NPIECE; i++)
-            if (on && (i * NS) / NPIECE == s) dma_piece(i, d);
+            if (on && ((i * NS) / NPIECE + KNN_FUSED_DMA_OFS) % NS == s) dma_piece(i, d);
     };
 
     // ---- one tile's MFMAs into X; in between, the fast test of the previous tile (Y): bit
