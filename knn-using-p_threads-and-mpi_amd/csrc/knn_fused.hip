@@ -542,8 +542,9 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                         thr = fminf(thr, fmaxf(lst[LL - 1], partner(lst[LL - 1])));
                     }
                 } else {
-                    const float wp = partner(w);  // the other half's candidate
-                    if (__ballot(w < INF || wp < INF)) {
+                    // (no lane inserting means no partner inserting: the swap waits for one)
+                    if (__ballot(w < INF)) {
+                        const float wp = partner(w);  // the other half's candidate
                         list_insert(w);
                         list_insert(wp);
                         thr = fminf(thr, lst[LL - 1]);
