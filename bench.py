@@ -3,12 +3,15 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config A|B|C|C1|L] [--no-cpu-baseline]
 
 One process per GPU (torchrun for N > 1).  Workload A (default, BASELINE configs[2]):
-1,000,000 train x 100,000 query rows per GPU x 128-d fp32, k = 10, 10 classes, synthetic
-rows from the counter-based generator generated directly in HBM.  The test
-set is sharded (rank r owns query rows [r*nq, (r+1)*nq)), train is replicated: weak
-scaling with no data-path collective (the reference's MPI_Gatherv of predictions,
-mpi.cpp:186, is not part of the timed region).  A "step" is one KNN(train, test, k) pass
-over the resident inputs: norms -> MFMA filter -> exact rescore/vote -> fallback.
+1,000,000 train x 100,000 query rows x 128-d fp32, k = 10, 10 classes, synthetic rows from
+the counter-based generator generated directly in HBM.  On N GPUs the fixed
+test set is split by the reference's rule (rank r owns shard_range(100k, N, r),
+multi-thread.cpp:154-158 / mpi.cpp:141-170) with train replicated: strong scaling with no
+data-path collective (the reference's MPI_Gatherv of predictions, mpi.cpp:186, is not part
+of the timed region).  --weak gives every rank 100,000 queries of its own instead.  A
+"step" is one KNN(train, test, k) pass over the resident inputs: norms -> MFMA filter ->
+exact rescore/vote -> fallback.  B (configs[3]) is the same split of 1M queries over a 4M-row
+train set.
 
 Config C (BASELINE configs[4]) is train-sharded: 32M bf16 train rows x 1M queries x
 256-d, k = 100; rank r owns train rows shard_range(32M, N, r) and every query, computes
@@ -43,7 +46,7 @@ sys.path.insert(0, REPO)
 
 CONFIGS = {
     # name: (n_train, n_query (per GPU when weak), d, k, classes, seed, scaling, dtype, sharding)
-    "A": (1_000_000, 100_000, 128, 10, 10, 1, "weak", "f32", "test"),
+    "A": (1_000_000, 100_000, 128, 10, 10, 1, "strong", "f32", "test"),
     "B": (4_000_000, 1_000_000, 64, 32, 10, 2, "strong", "f32", "test"),
     "C": (32_000_000, 1_000_000, 256, 100, 10, 3, "strong", "bf16", "train"),
     "C1": (4_000_000, 1_000_000, 256, 100, 10, 3, "strong", "bf16", "train"),
@@ -282,6 +285,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="A", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--weak", action="store_true",
+                    help="test-sharded configs: every rank owns n_query rows of its own (weak scaling)")
     ap.add_argument("--exchange", default="rccl", choices=["rccl", "torch"],
                     help="train-sharded configs: C-ABI RCCL communicator or torch.distributed all-to-all")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-buffer calls")
@@ -320,6 +325,8 @@ def main():
 
     nt, nq_cfg, d, k, C, seed, scaling, dtype, sharding = CONFIGS[args.config]
     nt, nq_cfg = args.nt or nt, args.nq or nq_cfg
+    if args.weak and sharding == "test":
+        scaling = "weak"
     kind = 1 if dtype == "bf16" else 0                  # bf16-exact generator values for bf16
     tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
     dev = torch.device("cuda", local)
@@ -350,11 +357,13 @@ def main():
     # ranks share a GPU: RCCL wants one rank per device)
     exchange = args.exchange if not share else "torch"
     comm = None
+    rccl_ranks = None
     if sharding == "train" and exchange == "rccl":
         uid = [knn.comm_unique_id() if rank == 0 else None]
         if world > 1:
             dist.broadcast_object_list(uid, src=0)
         comm = knn.Comm(ctx, uid[0], world, rank)
+        rccl_ranks = comm.count()  # ncclCommCount: the ranks RCCL itself sees
 
     def step():
         if sharding == "test":
@@ -478,6 +487,7 @@ def main():
             "stages_ms": {n: round(v, 3) for n, v in stages.items()},
             "gemm_stats": stats,
             "predictions_gathered": gathered,
+            "rccl_comm_ranks": rccl_ranks,
             "roofline": roof,
             "cpu_baseline": cpu,
             "select_stage": select,

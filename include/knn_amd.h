@@ -188,6 +188,10 @@ knn_status knn_merge_vote_device(knn_ctx* ctx, int32_t nsrc, int64_t nq, int32_t
  *     by (distance, global index) -- the reference's lower-index tie rule over the whole
  *     train set -- and votes.  d_pred (and optional d_dist / d_idx [owned][k]) receive the
  *     owned queries' results.  Collective: every rank calls it with the same test set and k.
+ *     A failure local to one rank (memory, its shard's arguments) is voted on by every rank
+ *     (one max-allreduce) before the exchange: the failing rank returns its own status, its
+ *     peers KNN_ERCCL, and no rank is left waiting inside the exchange.  With profile = 1 the
+ *     context's stage times hold the shard's stages, "exchange" and "merge_vote".
  *   knn_shard_range: the reference's contiguous split with the remainder on the last worker
  *     (multi-thread.cpp:154-158, mpi.cpp:141-170).
  *   knn_exchange_layout: element offsets / counts of the all-to-all for `rank` (int32
@@ -198,6 +202,8 @@ typedef struct knn_comm knn_comm;
 knn_status knn_comm_unique_id(void* id_out);
 knn_status knn_comm_create(knn_ctx* ctx, const void* id, int32_t nranks, int32_t rank, knn_comm** out);
 void knn_comm_destroy(knn_comm* comm);
+/* the number of ranks the RCCL communicator spans (ncclCommCount) */
+knn_status knn_comm_count(const knn_comm* comm, int32_t* nranks);
 knn_status knn_predict_train_sharded(knn_ctx* ctx, knn_comm* comm, const knn_dataset* train_shard, int64_t idx_base,
                                      const knn_dataset* test, int32_t k, int32_t num_classes, int32_t* d_pred,
                                      float* d_dist, int32_t* d_idx, void* hip_stream);

@@ -108,8 +108,13 @@ struct KnnPinnedAllocator {
     bool operator!=(const KnnPinnedAllocator<U>&) const { return false; }
 };
 
+// a process-unique id per flat view (knn_arff.cpp): the device contexts key their train
+// cache on it, never on an address the allocator can hand out again
+uint64_t knn_flat_view_uid();
+
 // Flat, KNN-ready view of a dataset (features [n][ld] row-major, ld = d rounded up to 4).
 struct KnnFlatView {
+    uint64_t uid = knn_flat_view_uid();
     std::vector<float, KnnPinnedAllocator<float>> feat;
     std::vector<int32_t, KnnPinnedAllocator<int32_t>> labels;   // (int)(float) of the class attribute (main.cpp:66)
     int64_t n = 0;

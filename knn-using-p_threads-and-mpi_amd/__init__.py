@@ -97,6 +97,7 @@ def load_library(path=LIB_PATH):
         "knn_comm_unique_id": (I32, [P]),
         "knn_comm_create": (I32, [P, P, I32, I32, ctypes.POINTER(P)]),
         "knn_comm_destroy": (None, [P]),
+        "knn_comm_count": (I32, [P, ctypes.POINTER(I32)]),
         "knn_predict_train_sharded": (I32, [P, P, DS, I64, DS, I32, I32, P, P, P, P]),
         "knn_shard_range": (I32, [I64, I32, I32, ctypes.POINTER(I64), ctypes.POINTER(I64)]),
         "knn_exchange_layout": (I32, [I64, I32, I32, I32, P, P, P, P]),
@@ -284,6 +285,11 @@ class Context:
         # cache_train: predict() keeps the device copy of train across calls (KNN_OPT_CACHE_TRAIN)
         opts = knn_opts(device, ALGOS[algo], train_splits, int(profile),
                         KNN_OPT_CACHE_TRAIN if cache_train else 0)
+        self.cache_train = bool(cache_train)
+        # the arrays whose addresses key the library's train cache (knn_predict): held until
+        # the next call replaces them, so no later array can be allocated at a cached address
+        # (_dataset copies inputs of another dtype or layout into temporaries)
+        self._train_key = None
         h = ctypes.c_void_p()
         st = self.lib.knn_create(ctypes.byref(h), ctypes.byref(opts))
         if st != KNN_OK:
@@ -318,6 +324,8 @@ class Context:
         pred = np.zeros(max(nq, 0), np.int32)
         dist = np.zeros((max(nq, 0), k), np.float32) if topk else None
         idx = np.zeros((max(nq, 0), k), np.int32) if topk else None
+        if self.cache_train:
+            self._train_key = keep1
         self._check(self.lib.knn_predict(self.h, ctypes.byref(tr), ctypes.byref(te), k, num_classes,
                                          q_begin, q_end, _ptr(pred), _ptr(dist), _ptr(idx)))
         return (pred, dist, idx) if topk else pred
@@ -489,6 +497,14 @@ class Comm:
         if st != KNN_OK:
             raise KnnError(st, self.lib.knn_last_error(self.ctx.h).decode())
         return q0, q1
+
+    def count(self):
+        """The number of ranks the RCCL communicator spans (knn_comm_count: ncclCommCount)."""
+        n = ctypes.c_int32()
+        st = self.lib.knn_comm_count(self.h, ctypes.byref(n))
+        if st != KNN_OK:
+            raise KnnError(st, "knn_comm_count")
+        return n.value
 
     def close(self):
         if getattr(self, "h", None):

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cmath>
 #include <cstdarg>
@@ -337,6 +338,15 @@ const char* kind_name(uint8_t k) {
     return k == K_STRING ? "STRING" : k == K_NOMINAL ? "NOMINAL" : k == K_MISSING ? "NUMERIC" : "FLOAT";
 }
 
+}  // namespace
+
+uint64_t knn_flat_view_uid() {
+    static std::atomic<uint64_t> next{1};
+    return next.fetch_add(1, std::memory_order_relaxed);
+}
+
+namespace {
+
 // Flatten features [0, na-1) and the class attribute with operator float semantics.
 void flatten(const ParsedArff& P, KnnFlatView* out) {
     const int na = (int)P.attrs.size();
@@ -420,7 +430,10 @@ void predict_range(ArffData* train, ArffData* test, int k, int64_t q0, int64_t q
         int32_t* dst = reinterpret_cast<int32_t*>(out) + (s - q0);
         auto job = [&, g, s, e, dst]() {
             std::lock_guard<std::mutex> busy(*devices().busy[g]);
-            st[g] = knn_predict(cs[g], &dtr, &dte, k, C, s, e, dst, nullptr, nullptr);
+            // the train cache hits only for this very flat view (a freed ArffData's buffers can
+            // be handed to the next one at the same address)
+            st[g] = knn_set_generation(cs[g], tr.uid);
+            if (st[g] == KNN_OK) st[g] = knn_predict(cs[g], &dtr, &dte, k, C, s, e, dst, nullptr, nullptr);
         };
         if (G == 1) job(); else th.emplace_back(job);
         s = e;

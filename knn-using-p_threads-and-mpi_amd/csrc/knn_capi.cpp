@@ -58,15 +58,13 @@ struct knn_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // device workspace
-    DBuf tnorm, tnp, qnorm, gthr, cnt, cand, fb_list, ctrl, timing;
+    DBuf tnorm, tnp, qnorm, gthr, cnt, cand, fb_list, ctrl, scratch;
     DBuf split_t, split_q;  // KNN_ALGO_GEMM_SPLIT / _BF16: bf16 [hi | lo] / rn copies of fp32 rows
+    DBuf pad_t;             // KNN_ALGO_GEMM, n_train not a multiple of 64: the rows padded to the tile grid
     DBuf seg_rec;           // k_direct_tile segment records [nseg][nq][3][k]
     DBuf tmax;              // fused filter: per-64-row train stats {max tn, max |t - rt|, max |rt|, 0}
     DBuf qstat;             // fused filter: per-query {|q|, |q - rq|} upper bounds
-    // kernel-study switches, read once from the environment in knn_create (never in a call)
-    int study_seed = 0, study_timing = 0, study_nofused = 0;
     int rescore_su = 0;  // test hook KNN_RESCORE_SU: the rescore's LDS staging size (0 = sized)
-    FilterStudy fstudy{0, {0}, -1, -1};
     // host-API staging (device copies of host inputs / outputs)
     DBuf h_train, h_labels, h_test, h_pred, h_dist, h_idx;
     int32_t* ctrl_host = nullptr;  // pinned: [0] status, [1] fallback count
@@ -112,6 +110,15 @@ knn_status fail(knn_ctx* c, knn_status s, const char* fmt, ...) {
         if (e__ != hipSuccess)                                                                  \
             return fail(ctx, e__ == hipErrorOutOfMemory ? KNN_ENOMEM : KNN_EHIP, "%s: %s (%s:%d)", \
                         #expr, hipGetErrorString(e__), __FILE__, __LINE__);                    \
+    } while (0)
+
+// HIP_OR_FAIL inside knn_predict's enqueue phase: drain and invalidate first (abort_call)
+#define HIP_OR_ABORT(expr)                                                                     \
+    do {                                                                                        \
+        hipError_t e__ = (expr);                                                                \
+        if (e__ != hipSuccess)                                                                  \
+            return abort_call(fail(c, e__ == hipErrorOutOfMemory ? KNN_ENOMEM : KNN_EHIP,       \
+                                   "%s: %s (%s:%d)", #expr, hipGetErrorString(e__), __FILE__, __LINE__)); \
     } while (0)
 
 // profiling helpers: events are created lazily and reused across calls
@@ -167,7 +174,7 @@ int choose_algo(const knn_ctx* c, int64_t nt, int64_t nq, int d, int k, int dtyp
     auto gemm_ok = [&](int algo) {
         const int fe = filter_elem(algo, dtype), rb = filter_row_bytes(fe, d);
         return knn_gemm_filter_supported(fe, rb) && k <= 128 && k <= nt &&
-               knn_gemm_filter_lds(fe, rb, k, &c->fstudy) <= 160 * 1024;
+               knn_gemm_filter_lds(fe, rb, k) <= 160 * 1024;
     };
     if (is_gemm(c->algo))
         return gemm_ok(c->algo) ? c->algo : KNN_ALGO_DIRECT;
@@ -352,8 +359,7 @@ int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int
     // tile; the slice gets a 1.5x margin.  Overflowing queries still finish exactly,
     // on the slow full-scan fallback.
     int occ = 1;
-    const hipError_t oe = fused ? knn_fused_occupancy(d, k, &occ, &c->fstudy)
-                                : knn_gemm_filter_occupancy(dtype, rb, k, &occ, &c->fstudy);
+    const hipError_t oe = fused ? knn_fused_occupancy(d, k, &occ) : knn_gemm_filter_occupancy(dtype, rb, k, &occ);
     if (oe != hipSuccess || occ < 1) occ = 1;
     const int64_t slots = (int64_t)occ * c->num_cus;
     int best = 1;
@@ -394,8 +400,8 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     HIP_OR_FAIL(c, c->fb_list.ensure(sizeof(int32_t) * nq));
 
     // bf16 MFMA operands (rounded fp32 rows or bf16 data) run the fused-norm filter
-    const bool fused = !c->study_nofused && (felem == ELEM_ROUND || felem == ELEM_BF16) &&
-                       knn_fused_supported(d) && knn_fused_plan(d, k, &c->fstudy).nw > 0;
+    const bool fused = (felem == ELEM_ROUND || felem == ELEM_BF16) && knn_fused_supported(d) &&
+                       knn_fused_plan(d, k).nw > 0;
     float coef, eta;
     if (fused) {
         certificate_fused(d, felem == ELEM_ROUND, &coef, &eta);
@@ -419,61 +425,57 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     stage_begin(c, st, gate ? "filter_init_rerun" : "filter_init");
     HIP_OR_FAIL(c, knn_launch_fill_u32(c->gthr.as<uint32_t>(), nq, 0xFF800000u, gate, st));  // ordered(+inf)
     stage_end(c, st);
-    // study option KNN_FILTER_SEED=1: starting thresholds from the exact k-th distance to a
-    // spread sample of train rows (k_seed_threshold), so the first segment does not begin
-    // with all-passing tiles.  Measured (same box): candidates -18 % on A, -17 % on B, -24 %
-    // on C1, but the filter time is unchanged (36.2 vs 36.2 ms on A) and the seed costs
-    // 1.4-1.8 ms, so it is off by default: the slow path's cost is its per-tile calls on the
-    // long tail, not the heap-filling phase.
-    const int64_t ns = std::min<int64_t>(nt, std::min<int64_t>(KNN_SEED_MAX_ROWS, std::max<int64_t>(256, 16 * (int64_t)k)));
-    if (c->study_seed == 1 && ns >= k) {
-        SeedArgs sa{};
-        sa.train = tr->feat; sa.nt = nt; sa.ld_t = tr->ld;
-        sa.test = te->feat; sa.nq = nq; sa.ld_q = te->ld; sa.d = d; sa.k = k;
-        sa.ns = (int)ns; sa.ld_lds = (d + 3) & ~3;
-        sa.gthr = c->gthr.as<uint32_t>();
-        stage_begin(c, st, gate ? "seed_rerun" : "seed");
-        HIP_OR_FAIL(c, knn_launch_seed_threshold(sa, dtype, st));
-        stage_end(c, st);
-    }
 
-    // filter operands: the rows themselves, or their bf16 [hi | lo] split (2d elements per row)
+    // filter operands: the rows themselves, or their bf16 [hi | lo] split (2d elements per row);
+    // train operand rows always cover the 64-row tile grid (ntp rows)
+    const int64_t ntp = (nt + 63) / 64 * 64;
     const void* ftrain = tr->feat;
     const void* ftest = te->feat;
     int fld_t = tr->ld, fld_q = te->ld;
     if (fused) {
         // augmented bf16 rows: train [rn(t) | tn split], queries [-2 rn(q) | 1 1 1]
-        HIP_OR_FAIL(c, c->split_t.ensure(sizeof(uint16_t) * (size_t)(d + 16) * nt));
+        // (pad rows: zero features, a huge norm -- they never pass)
+        HIP_OR_FAIL(c, c->split_t.ensure(sizeof(uint16_t) * (size_t)(d + 16) * ntp));
         HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * (size_t)(d + 16) * nq));
         stage_begin(c, st, gate ? "aug_rerun" : "aug");
-        HIP_OR_FAIL(c, knn_launch_aug_rows(tr->feat, dtype, nt, tr->ld, d, c->tnorm.as<float>(), 1.0f,
+        HIP_OR_FAIL(c, knn_launch_aug_rows(tr->feat, dtype, ntp, nt, tr->ld, d, c->tnorm.as<float>(), 1.0f,
                                            c->split_t.as<uint16_t>(), st, gate));
-        HIP_OR_FAIL(c, knn_launch_aug_rows(te->feat, dtype, nq, te->ld, d, nullptr, -2.0f,
+        HIP_OR_FAIL(c, knn_launch_aug_rows(te->feat, dtype, nq, nq, te->ld, d, nullptr, -2.0f,
                                            c->split_q.as<uint16_t>(), st, gate));
         stage_end(c, st);
         ftrain = c->split_t.p; ftest = c->split_q.p;
         fld_t = fld_q = d + 16;
     } else if (felem == ELEM_SPLIT) {
-        HIP_OR_FAIL(c, c->split_t.ensure(sizeof(uint16_t) * 2 * d * nt));
+        HIP_OR_FAIL(c, c->split_t.ensure(sizeof(uint16_t) * 2 * d * ntp));
         HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * 2 * d * nq));
         stage_begin(c, st, gate ? "split_rerun" : "split");
+        HIP_OR_FAIL(c, hipMemsetAsync(c->split_t.as<uint16_t>() + 2 * d * nt, 0, sizeof(uint16_t) * 2 * d * (ntp - nt), st));
         HIP_OR_FAIL(c, knn_launch_split_rows((const float*)tr->feat, nt, tr->ld, d, c->split_t.as<uint16_t>(), st, gate));
         HIP_OR_FAIL(c, knn_launch_split_rows((const float*)te->feat, nq, te->ld, d, c->split_q.as<uint16_t>(), st, gate));
         stage_end(c, st);
         ftrain = c->split_t.p; ftest = c->split_q.p;
         fld_t = fld_q = 2 * d;
     } else if (felem == ELEM_ROUND) {
-        HIP_OR_FAIL(c, c->split_t.ensure(sizeof(uint16_t) * d * nt));
+        HIP_OR_FAIL(c, c->split_t.ensure(sizeof(uint16_t) * d * ntp));
         HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * d * nq));
         stage_begin(c, st, gate ? "round_rerun" : "round");
+        HIP_OR_FAIL(c, hipMemsetAsync(c->split_t.as<uint16_t>() + d * nt, 0, sizeof(uint16_t) * d * (ntp - nt), st));
         HIP_OR_FAIL(c, knn_launch_round_rows((const float*)tr->feat, nt, tr->ld, d, c->split_t.as<uint16_t>(), st, gate));
         HIP_OR_FAIL(c, knn_launch_round_rows((const float*)te->feat, nq, te->ld, d, c->split_q.as<uint16_t>(), st, gate));
         stage_end(c, st);
         ftrain = c->split_t.p; ftest = c->split_q.p;
         fld_t = fld_q = d;
+    } else if (nt % 64) {
+        // the caller's rows, copied onto the 64-row tile grid: every tile the filter copies
+        // into LDS is whole (one DMA form, knn_kernels.hip), the pad rows never pass (+inf norms)
+        const size_t es = (size_t)elem_size(dtype), pitch = es * (size_t)tr->ld;
+        HIP_OR_FAIL(c, c->pad_t.ensure(pitch * (size_t)ntp));
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->pad_t.p, tr->feat, pitch * (size_t)nt, hipMemcpyDeviceToDevice, st));
+        HIP_OR_FAIL(c, hipMemsetAsync((unsigned char*)c->pad_t.p + pitch * (size_t)nt, 0, pitch * (size_t)(ntp - nt), st));
+        ftrain = c->pad_t.p;
     }
 
-    const FilterPlan plan = fused ? knn_fused_plan(d, k, &c->fstudy) : knn_gemm_filter_plan(kelem, rb, k, &c->fstudy);
+    const FilterPlan plan = fused ? knn_fused_plan(d, k) : knn_gemm_filter_plan(kelem, rb, k);
     const int64_t n_qtiles = (nq + plan.bm - 1) / plan.bm;
     GemmFilterArgs g{};
     g.nt = nt; g.n_qtiles = (int)n_qtiles;
@@ -482,7 +484,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     int nseg = 0;
     if (fused && c->train_splits <= 0) {
         int occ = 1;
-        if (knn_fused_occupancy(d, k, &occ, &c->fstudy) != hipSuccess || occ < 1) occ = 1;
+        if (knn_fused_occupancy(d, k, &occ) != hipSuccess || occ < 1) occ = 1;
         int nb = 1;
         knn_fused_schedule(g, occ * c->num_cus, &nb);
         if (nb <= max_splits(nt, k, cap)) nseg = nb;
@@ -505,29 +507,12 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     g.qstat = fused ? c->qstat.as<float2>() : nullptr;
     g.status = c->ctrl.as<int32_t>();
     g.gate = gate;
-    // kernel studies: KNN_FILTER_TIMING=1 with a -DKNN_FILTER_TIMING build prints the
-    // filter's per-phase shader clocks per wave (wait+barrier, DMA issue, step, slow path)
-    const bool timing = c->study_timing != 0;
-    if (timing) {
-        HIP_OR_FAIL(c, c->timing.ensure(16 * sizeof(unsigned long long)));
-        HIP_OR_FAIL(c, hipMemsetAsync(c->timing.p, 0, 16 * sizeof(unsigned long long), st));
-        g.timing = c->timing.as<unsigned long long>();
-    }
     if (fused && g.g2 >= 0 && nseg > 1)  // whole query tiles write only sub-slice 0
         HIP_OR_FAIL(c, hipMemsetAsync(c->cnt.p, 0, sizeof(int32_t) * 2 * nseg * nq, st));
     stage_begin(c, st, gate ? "gemm_filter_rerun" : "gemm_filter");
-    if (fused) HIP_OR_FAIL(c, knn_launch_fused(g, st, &c->fstudy));
-    else HIP_OR_FAIL(c, knn_launch_gemm_filter(g, kelem, rb, st, &c->fstudy));
+    if (fused) HIP_OR_FAIL(c, knn_launch_fused(g, st));
+    else HIP_OR_FAIL(c, knn_launch_gemm_filter(g, kelem, rb, st));
     stage_end(c, st);
-    if (timing) {
-        unsigned long long t[16];
-        HIP_OR_FAIL(c, hipMemcpyAsync(t, c->timing.p, sizeof(t), hipMemcpyDeviceToHost, st));
-        HIP_OR_FAIL(c, hipStreamSynchronize(st));
-        const double w = t[4] ? (double)t[4] : 1.0;
-        fprintf(stderr, "[knn filter timing] waves=%llu clocks/wave: wait+barrier %.4g  dma %.4g  step %.4g  slow %.4g"
-                " ([5] %.4g; [6] %.4g, [7] %.4g, [8] %.4g)\n", t[4], t[0] / w, t[1] / w,
-                t[2] / w, t[3] / w, t[5] / w, t[6] / w, t[7] / w, t[8] / w);
-    }
 
     RescoreArgs r{};
     r.train = tr->feat; r.labels = tr->labels; r.ld_t = tr->ld;
@@ -581,15 +566,8 @@ knn_status knn_create(knn_ctx** out, const knn_opts* opts) {
         c->profile = opts->profile;
         c->cache_train = (opts->flags & KNN_OPT_CACHE_TRAIN) != 0;
     }
-    // kernel-study switches (DESIGN.md "Ablation builds"): read here once, never per call
-    if (const char* e = getenv("KNN_FILTER_SEED")) c->study_seed = atoi(e);
-    if (getenv("KNN_FILTER_TIMING")) c->study_timing = 1;
-    if (const char* e = getenv("KNN_FILTER_FUSED")) c->study_nofused = atoi(e) == 0;
-    if (const char* e = getenv("KNN_FILTER_NBUF")) c->fstudy.nbuf = atoi(e);
-    if (const char* e = getenv("KNN_FILTER_PSTEP")) c->fstudy.pstep = atoi(e);
-    if (const char* e = getenv("KNN_FILTER_KR")) c->fstudy.kr = atoi(e);
+    // test hook: the rescore's LDS staging size (read here once, never per call)
     if (const char* e = getenv("KNN_RESCORE_SU")) c->rescore_su = atoi(e);
-    if (const char* e = getenv("KNN_FILTER_SHAPE")) snprintf(c->fstudy.shape, sizeof(c->fstudy.shape), "%s", e);
     if (c->device < 0 || c->device >= ndev) { delete c; return KNN_ENODEV; }
     hipDeviceProp_t prop;
     if (hipSetDevice(c->device) != hipSuccess || hipGetDeviceProperties(&prop, c->device) != hipSuccess) {
@@ -631,7 +609,7 @@ void knn_destroy(knn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (DBuf* b : {&c->tnorm, &c->tnp, &c->qnorm, &c->gthr, &c->cnt, &c->cand,
-                    &c->fb_list, &c->ctrl, &c->timing, &c->split_t, &c->split_q, &c->seg_rec, &c->tmax, &c->qstat, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
+                    &c->fb_list, &c->ctrl, &c->scratch, &c->split_t, &c->split_q, &c->pad_t, &c->seg_rec, &c->tmax, &c->qstat, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
                     &c->h_dist, &c->h_idx})
         b->release();
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
@@ -653,6 +631,10 @@ const char* knn_last_error(const knn_ctx* c) { return c ? c->err.c_str() : "null
 
 int knn_ctx_device(const knn_ctx* c) { return c->device; }
 void* knn_ctx_stream(const knn_ctx* c) { return (void*)c->stream; }
+void knn_ctx_stage_begin(knn_ctx* c, void* stream, const char* name);
+void knn_ctx_stage_end(knn_ctx* c, void* stream);
+knn_status knn_merge_vote_append(knn_ctx* c, int32_t nsrc, int64_t nq, int32_t k, int32_t C, const int32_t* d_rec,
+                                 int32_t* d_pred, float* d_dist, int32_t* d_idx, void* hip_stream);
 
 namespace {
 
@@ -840,12 +822,21 @@ knn_status knn_merge_vote_device(knn_ctx* c, int32_t nsrc, int64_t nq, int32_t k
                                  void* hip_stream) {
     if (!c) return KNN_EINVAL;
     c->err.clear();
+    c->stages.clear();
+    return knn_merge_vote_append(c, nsrc, nq, k, C, d_rec, d_pred, d_dist, d_idx, hip_stream);
+}
+
+}  // extern "C"
+
+// the merge, with its stage appended to the context's profile (knn_predict_train_sharded
+// keeps the shard's filter / rescore stages and the exchange beside it)
+knn_status knn_merge_vote_append(knn_ctx* c, int32_t nsrc, int64_t nq, int32_t k, int32_t C, const int32_t* d_rec,
+                                 int32_t* d_pred, float* d_dist, int32_t* d_idx, void* hip_stream) {
     if (nsrc < 1 || nq < 0 || k < 1 || k > 1024 || C < 1 || C > 16384)
         return fail(c, KNN_EINVAL, "merge: bad nsrc=%d nq=%lld k=%d C=%d", nsrc, (long long)nq, k, C);
     if (nq > 0 && (!d_rec || !d_pred)) return fail(c, KNN_EINVAL, "merge: d_rec / d_pred is NULL");
     HIP_OR_FAIL(c, hipSetDevice(c->device));
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
-    c->stages.clear();
     if (nq == 0) return KNN_OK;
     HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st));
     MergeArgs m{};
@@ -857,6 +848,8 @@ knn_status knn_merge_vote_device(knn_ctx* c, int32_t nsrc, int64_t nq, int32_t k
     stage_end(c, st);
     return finish_call(c, st);
 }
+
+extern "C" {
 
 knn_status knn_predict(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int32_t k, int32_t C,
                        int64_t q_begin, int64_t q_end, int32_t* out_pred, float* out_dist,
@@ -878,10 +871,9 @@ knn_status knn_predict(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te,
     if (!out_pred) return fail(c, KNN_EINVAL, "out_pred is NULL");
     HIP_OR_FAIL(c, hipSetDevice(c->device));
     hipStream_t st = c->stream, cs = c->cstream;
-    knn_dataset dtr;
-    if ((s = train_device(c, tr, st, &dtr)) != KNN_OK) return s;
-    const int d = tr->d, ldd = dtr.ld;
+    const int d = tr->d;
     const size_t es = (size_t)elem_size(tr->dtype);
+    const int ldd = (int)((d + (int)(16 / es) - 1) / (int)(16 / es) * (int)(16 / es));  // device rows padded to 16 B
     const int algo = choose_algo(c, tr->n, nq, d, k, tr->dtype);
     const bool gemm = is_gemm(algo);
     // queries stream through two device slots: batch b+1 uploads (copy stream) while batch b
@@ -889,56 +881,73 @@ knn_status knn_predict(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te,
     int64_t B = std::min<int64_t>(nq, c->batch_rows);
     if (gemm) B = std::min<int64_t>(B, c->ws_queries);
     const int64_t nb = (nq + B - 1) / B;
+    {
+        // the device call's checks on the shapes it will see, before anything is enqueued: no
+        // early return may leave a copy to or from the caller's buffers in flight
+        const knn_dataset vtr{(const void*)(uintptr_t)256, tr->labels, tr->n, d, ldd, tr->dtype};
+        const knn_dataset vq{(const void*)(uintptr_t)256, nullptr, B, d, ldd, te->dtype};
+        const QueryOut vo{out_pred, out_dist, out_idx, nullptr, k, 0};
+        if ((s = validate_call(c, &vtr, &vq, k, C, vo, false)) != KNN_OK) return s;
+    }
+    // from here on every error drains both streams (no DMA outlives the call) and drops the
+    // train cache entry (its upload may not have run)
+    auto abort_call = [&](knn_status e) {
+        (void)hipStreamSynchronize(cs);
+        (void)hipStreamSynchronize(st);
+        c->tcache.valid = false;
+        return e;
+    };
+    knn_dataset dtr;
+    if ((s = train_device(c, tr, st, &dtr)) != KNN_OK) return abort_call(s);
     for (int i = 0; i < 2 && i < nb; i++) {
-        HIP_OR_FAIL(c, c->q_slot[i].ensure(es * (size_t)ldd * B));
-        HIP_OR_FAIL(c, c->pred_slot[i].ensure(sizeof(int32_t) * B));
-        if (out_dist) HIP_OR_FAIL(c, c->dist_slot[i].ensure(sizeof(float) * B * k));
-        if (out_idx) HIP_OR_FAIL(c, c->idx_slot[i].ensure(sizeof(int32_t) * B * k));
+        HIP_OR_ABORT(c->q_slot[i].ensure(es * (size_t)ldd * B));
+        HIP_OR_ABORT(c->pred_slot[i].ensure(sizeof(int32_t) * B));
+        if (out_dist) HIP_OR_ABORT(c->dist_slot[i].ensure(sizeof(float) * B * k));
+        if (out_idx) HIP_OR_ABORT(c->idx_slot[i].ensure(sizeof(int32_t) * B * k));
     }
     while ((int64_t)c->ctrl_slots.size() < nb) {
         int32_t* p = nullptr;
-        HIP_OR_FAIL(c, hipHostMalloc((void**)&p, 4 * sizeof(int32_t), hipHostMallocDefault));
+        HIP_OR_ABORT(hipHostMalloc((void**)&p, 4 * sizeof(int32_t), hipHostMallocDefault));
         c->ctrl_slots.push_back(p);
     }
     auto rows = [&](int64_t b) { return std::min(B, nq - b * B); };
     auto upload = [&](int64_t b) -> knn_status {
         const int sl = (int)(b & 1);
         const unsigned char* src = (const unsigned char*)te->feat + es * (size_t)(q_begin + b * B) * (size_t)te->ld;
-        HIP_OR_FAIL(c, hipMemcpy2DAsync(c->q_slot[sl].p, es * ldd, src, es * te->ld, es * d, rows(b),
+        HIP_OR_ABORT(hipMemcpy2DAsync(c->q_slot[sl].p, es * ldd, src, es * te->ld, es * d, rows(b),
                                         hipMemcpyHostToDevice, cs));
-        HIP_OR_FAIL(c, hipEventRecord(c->ev_up[sl], cs));
+        HIP_OR_ABORT(hipEventRecord(c->ev_up[sl], cs));
         c->stats[7] += (int64_t)(es * d * rows(b));
         return KNN_OK;
     };
-    if ((s = upload(0)) != KNN_OK) return s;
+    if ((s = upload(0)) != KNN_OK) return abort_call(s);
     for (int64_t b = 0; b < nb; b++) {
         const int sl = (int)(b & 1);
-        HIP_OR_FAIL(c, hipStreamWaitEvent(st, c->ev_up[sl], 0));
-        if (b >= 2) HIP_OR_FAIL(c, hipStreamWaitEvent(st, c->ev_down[sl], 0));  // output slot downloaded
+        HIP_OR_ABORT(hipStreamWaitEvent(st, c->ev_up[sl], 0));
+        if (b >= 2) HIP_OR_ABORT(hipStreamWaitEvent(st, c->ev_down[sl], 0));  // output slot downloaded
         const knn_dataset dq{c->q_slot[sl].p, nullptr, rows(b), d, ldd, te->dtype};
         const QueryOut o{c->pred_slot[sl].as<int32_t>(), out_dist ? c->dist_slot[sl].as<float>() : nullptr,
                          out_idx ? c->idx_slot[sl].as<int32_t>() : nullptr, nullptr, k, 0};
-        if (b == 0 && (s = validate_call(c, &dtr, &dq, k, C, o, false)) != KNN_OK) return s;
-        if ((s = predict_enqueue(c, &dtr, &dq, k, C, o, st, algo, c->ctrl_slots[b])) != KNN_OK) return s;
-        HIP_OR_FAIL(c, hipEventRecord(c->ev_done[sl], st));
+        if ((s = predict_enqueue(c, &dtr, &dq, k, C, o, st, algo, c->ctrl_slots[b])) != KNN_OK) return abort_call(s);
+        HIP_OR_ABORT(hipEventRecord(c->ev_done[sl], st));
         if (b + 1 < nb) {
-            if (b + 1 >= 2) HIP_OR_FAIL(c, hipStreamWaitEvent(cs, c->ev_done[(b + 1) & 1], 0));  // slot free
-            if ((s = upload(b + 1)) != KNN_OK) return s;
+            if (b + 1 >= 2) HIP_OR_ABORT(hipStreamWaitEvent(cs, c->ev_done[(b + 1) & 1], 0));  // slot free
+            if ((s = upload(b + 1)) != KNN_OK) return abort_call(s);
         }
-        HIP_OR_FAIL(c, hipStreamWaitEvent(cs, c->ev_done[sl], 0));
+        HIP_OR_ABORT(hipStreamWaitEvent(cs, c->ev_done[sl], 0));
         const int64_t q0 = b * B;
-        HIP_OR_FAIL(c, hipMemcpyAsync(out_pred + q0, c->pred_slot[sl].p, sizeof(int32_t) * rows(b),
+        HIP_OR_ABORT(hipMemcpyAsync(out_pred + q0, c->pred_slot[sl].p, sizeof(int32_t) * rows(b),
                                       hipMemcpyDeviceToHost, cs));
         if (out_dist)
-            HIP_OR_FAIL(c, hipMemcpyAsync(out_dist + q0 * k, c->dist_slot[sl].p, sizeof(float) * rows(b) * k,
+            HIP_OR_ABORT(hipMemcpyAsync(out_dist + q0 * k, c->dist_slot[sl].p, sizeof(float) * rows(b) * k,
                                           hipMemcpyDeviceToHost, cs));
         if (out_idx)
-            HIP_OR_FAIL(c, hipMemcpyAsync(out_idx + q0 * k, c->idx_slot[sl].p, sizeof(int32_t) * rows(b) * k,
+            HIP_OR_ABORT(hipMemcpyAsync(out_idx + q0 * k, c->idx_slot[sl].p, sizeof(int32_t) * rows(b) * k,
                                           hipMemcpyDeviceToHost, cs));
-        HIP_OR_FAIL(c, hipEventRecord(c->ev_down[sl], cs));
+        HIP_OR_ABORT(hipEventRecord(c->ev_down[sl], cs));
     }
-    HIP_OR_FAIL(c, hipStreamSynchronize(cs));
-    HIP_OR_FAIL(c, hipStreamSynchronize(st));
+    HIP_OR_ABORT(hipStreamSynchronize(cs));
+    HIP_OR_ABORT(hipStreamSynchronize(st));
     collect_stages(c);
     for (int64_t b = 0; b < nb; b++) {
         if ((s = check_status(c, c->ctrl_slots[b])) != KNN_OK) return s;
@@ -1026,8 +1035,8 @@ knn_status knn_confusion_matrix_device(knn_ctx* c, const int32_t* d_pred, const 
     HIP_OR_FAIL(c, hipMemsetAsync(d_cm, 0, sizeof(int32_t) * (size_t)C * (size_t)C, st));
     unsigned long long* corr = reinterpret_cast<unsigned long long*>(d_correct);
     if (!corr) {
-        HIP_OR_FAIL(c, c->timing.ensure(16 * sizeof(unsigned long long)));  // scratch word
-        corr = c->timing.as<unsigned long long>() + 15;
+        HIP_OR_FAIL(c, c->scratch.ensure(sizeof(unsigned long long)));  // scratch word
+        corr = c->scratch.as<unsigned long long>();
     }
     HIP_OR_FAIL(c, hipMemsetAsync(corr, 0, sizeof(unsigned long long), st));
     stage_begin(c, st, "confusion");
@@ -1056,3 +1065,6 @@ float knn_accuracy(const int32_t* cm, int32_t C, int64_t n) {
 }
 
 }  // extern "C"
+
+void knn_ctx_stage_begin(knn_ctx* c, void* stream, const char* name) { stage_begin(c, (hipStream_t)stream, name); }
+void knn_ctx_stage_end(knn_ctx* c, void* stream) { stage_end(c, (hipStream_t)stream); }

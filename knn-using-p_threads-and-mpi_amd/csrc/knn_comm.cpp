@@ -26,9 +26,13 @@
 
 #include "../../include/knn_amd.h"
 
-// context accessors (knn_capi.cpp)
+// context internals (knn_capi.cpp)
 int knn_ctx_device(const knn_ctx* c);
 void* knn_ctx_stream(const knn_ctx* c);
+void knn_ctx_stage_begin(knn_ctx* c, void* stream, const char* name);
+void knn_ctx_stage_end(knn_ctx* c, void* stream);
+knn_status knn_merge_vote_append(knn_ctx* c, int32_t nsrc, int64_t nq, int32_t k, int32_t C, const int32_t* d_rec,
+                                 int32_t* d_pred, float* d_dist, int32_t* d_idx, void* hip_stream);
 
 namespace {
 
@@ -41,6 +45,8 @@ struct Rccl {
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclSend) send = nullptr;
     decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclCommCount) comm_count = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
     std::string err;
 };
@@ -65,9 +71,12 @@ Rccl& rccl() {
         KNN_RCCL_SYM(group_end, "ncclGroupEnd");
         KNN_RCCL_SYM(send, "ncclSend");
         KNN_RCCL_SYM(recv, "ncclRecv");
+        KNN_RCCL_SYM(all_reduce, "ncclAllReduce");
+        KNN_RCCL_SYM(comm_count, "ncclCommCount");
         KNN_RCCL_SYM(error_string, "ncclGetErrorString");
 #undef KNN_RCCL_SYM
-        if (!r.get_unique_id || !r.init_rank || !r.destroy || !r.group_start || !r.group_end || !r.send || !r.recv)
+        if (!r.get_unique_id || !r.init_rank || !r.destroy || !r.group_start || !r.group_end || !r.send || !r.recv ||
+            !r.all_reduce || !r.comm_count)
             r.err = "RCCL lacks a required symbol";
     });
     return r;
@@ -89,6 +98,8 @@ struct knn_comm {
     size_t rec_bytes = 0;
     void* lists = nullptr;
     size_t lists_bytes = 0;
+    int32_t* flag = nullptr;       // device word of the per-call failure vote (allocated at create)
+    int32_t* flag_host = nullptr;  // pinned copy of the vote's result
     std::string err;
 };
 
@@ -160,13 +171,28 @@ knn_status knn_comm_create(knn_ctx* ctx, const void* id, int32_t nranks, int32_t
         delete c;
         return KNN_EHIP;
     }
+    // the failure vote's words exist before any call, so a call never fails to take part in it
+    if (hipMalloc((void**)&c->flag, sizeof(int32_t)) != hipSuccess ||
+        hipHostMalloc((void**)&c->flag_host, sizeof(int32_t), hipHostMallocDefault) != hipSuccess) {
+        knn_comm_destroy(c);
+        return KNN_ENOMEM;
+    }
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
     if (rccl().init_rank(&c->comm, nranks, uid, rank) != ncclSuccess) {
-        delete c;
+        c->comm = nullptr;
+        knn_comm_destroy(c);
         return KNN_ERCCL;
     }
     *out = c;
+    return KNN_OK;
+}
+
+knn_status knn_comm_count(const knn_comm* c, int32_t* nranks) {
+    if (!c || !nranks || !c->comm) return KNN_EINVAL;
+    int n = 0;
+    if (rccl().comm_count(c->comm, &n) != ncclSuccess) return KNN_ERCCL;
+    *nranks = n;
     return KNN_OK;
 }
 
@@ -176,47 +202,64 @@ void knn_comm_destroy(knn_comm* c) {
     if (c->comm && rccl_ok()) (void)rccl().destroy(c->comm);
     if (c->rec) (void)hipFree(c->rec);
     if (c->lists) (void)hipFree(c->lists);
+    if (c->flag) (void)hipFree(c->flag);
+    if (c->flag_host) (void)hipHostFree(c->flag_host);
     delete c;
 }
 
 knn_status knn_predict_train_sharded(knn_ctx* ctx, knn_comm* comm, const knn_dataset* shard, int64_t idx_base,
                                      const knn_dataset* test, int32_t k, int32_t num_classes, int32_t* d_pred,
                                      float* d_dist, int32_t* d_idx, void* hip_stream) {
+    // arguments every rank passes alike (collective contract): a bad one fails on every rank
+    // before any collective
     if (!ctx || !comm || !shard || !test) return KNN_EINVAL;
-    if (k < 1 || k > 1024) return KNN_EINVAL;
+    if (k < 1 || k > 1024 || comm->nranks > 1024) return KNN_EINVAL;
     const int64_t nq = test->n;
     int64_t m0, m1;
     knn_shard_range(nq, comm->nranks, comm->rank, &m0, &m1);
-    if (m1 > m0 && !d_pred) return KNN_EINVAL;
     if (hipSetDevice(comm->device) != hipSuccess) return KNN_EHIP;
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : (hipStream_t)knn_ctx_stream(ctx);
     const size_t row = 3 * (size_t)k * sizeof(int32_t);
-    if (grow(&comm->rec, &comm->rec_bytes, row * (size_t)std::max<int64_t>(nq, 1)) != hipSuccess) return KNN_ENOMEM;
-    if (grow(&comm->lists, &comm->lists_bytes, row * (size_t)std::max<int64_t>(m1 - m0, 1) * comm->nranks) != hipSuccess)
-        return KNN_ENOMEM;
-    // 1. this rank's shard: exact top-k of every query, records with global indices
-    knn_status s = knn_shard_topk_device(ctx, shard, test, k, num_classes, idx_base, (int32_t*)comm->rec, st);
-    if (s != KNN_OK) return s;
-    // 2. all-to-all of the records: rank b receives the rows of its own queries from everyone
-    int64_t so[1024], sc[1024], ro[1024], rc[1024];
-    if (comm->nranks > 1024) return KNN_EINVAL;
-    knn_exchange_layout(nq, k, comm->nranks, comm->rank, so, sc, ro, rc);
+    // 1. this rank's shard: exact top-k of every query, records with global indices.  A
+    //    failure here is local (memory, this rank's arguments): it is not returned yet
+    knn_status s = KNN_OK;
+    if (m1 > m0 && !d_pred) s = KNN_EINVAL;
+    if (s == KNN_OK && (grow(&comm->rec, &comm->rec_bytes, row * (size_t)std::max<int64_t>(nq, 1)) != hipSuccess ||
+                        grow(&comm->lists, &comm->lists_bytes,
+                             row * (size_t)std::max<int64_t>(m1 - m0, 1) * comm->nranks) != hipSuccess))
+        s = KNN_ENOMEM;
+    if (s == KNN_OK) s = knn_shard_topk_device(ctx, shard, test, k, num_classes, idx_base, (int32_t*)comm->rec, st);
+    // 2. every rank votes on whether all shards succeeded (a max-allreduce of one word), so a
+    //    rank that failed locally still meets its peers here and all of them return instead of
+    //    one leaving the others blocked inside the exchange
     Rccl& r = rccl();
+    const int32_t mine = s == KNN_OK ? 0 : 1;
+    if (hipMemcpyAsync(comm->flag, &mine, sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
+        r.all_reduce(comm->flag, comm->flag, 1, ncclInt32, ncclMax, comm->comm, st) != ncclSuccess ||
+        hipMemcpyAsync(comm->flag_host, comm->flag, sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return KNN_ERCCL;
+    if (s != KNN_OK) return s;
+    if (*comm->flag_host != 0) return KNN_ERCCL;  // a peer's shard failed
+    // 3. all-to-all of the records: rank b receives the rows of its own queries from everyone
+    int64_t so[1024], sc[1024], ro[1024], rc[1024];
+    knn_exchange_layout(nq, k, comm->nranks, comm->rank, so, sc, ro, rc);
+    knn_ctx_stage_begin(ctx, st, "exchange");
     if (r.group_start() != ncclSuccess) return KNN_ERCCL;
-    for (int32_t b = 0; b < comm->nranks; b++) {
-        if (sc[b] > 0 && r.send((const int32_t*)comm->rec + so[b], (size_t)sc[b], ncclInt32, b, comm->comm, st) != ncclSuccess) {
-            r.group_end();
-            return KNN_ERCCL;
-        }
-        if (rc[b] > 0 && r.recv((int32_t*)comm->lists + ro[b], (size_t)rc[b], ncclInt32, b, comm->comm, st) != ncclSuccess) {
-            r.group_end();
-            return KNN_ERCCL;
-        }
+    bool ok = true;
+    for (int32_t b = 0; b < comm->nranks && ok; b++) {
+        if (sc[b] > 0 && r.send((const int32_t*)comm->rec + so[b], (size_t)sc[b], ncclInt32, b, comm->comm, st) != ncclSuccess)
+            ok = false;
+        if (ok && rc[b] > 0 &&
+            r.recv((int32_t*)comm->lists + ro[b], (size_t)rc[b], ncclInt32, b, comm->comm, st) != ncclSuccess)
+            ok = false;
     }
-    if (r.group_end() != ncclSuccess) return KNN_ERCCL;
-    // 3. merge + vote of the owned queries (ordered by distance, then global index)
+    if (r.group_end() != ncclSuccess || !ok) return KNN_ERCCL;
+    knn_ctx_stage_end(ctx, st);
+    // 4. merge + vote of the owned queries (ordered by distance, then global index); the
+    //    shard's stage times stay in the context's profile beside the exchange and the merge
     if (m1 == m0) return hipStreamSynchronize(st) == hipSuccess ? KNN_OK : KNN_EHIP;
-    return knn_merge_vote_device(ctx, comm->nranks, m1 - m0, k, num_classes, (const int32_t*)comm->lists, d_pred,
+    return knn_merge_vote_append(ctx, comm->nranks, m1 - m0, k, num_classes, (const int32_t*)comm->lists, d_pred,
                                  d_dist, d_idx, st);
 }
 

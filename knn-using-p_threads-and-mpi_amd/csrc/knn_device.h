@@ -30,9 +30,41 @@ __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 __device__ __forceinline__ u64 umin64(u64 a, u64 b) { return a < b ? a : b; }
 __device__ __forceinline__ u64 umax64(u64 a, u64 b) { return a < b ? b : a; }
 
+// The word of lane ^ j (j a power of two <= 32, a constant once the networks below are
+// unrolled), without ds_bpermute: j = 1, 2 by a DPP quad permutation, j = 4, 8 by two DPP
+// row shifts (row_shl / row_shr: the partner sits j lanes up or down inside its row of 16)
+// and a select, j = 16 by ds_swizzle's xor mode (no address operand), j = 32 by
+// v_permlane32_swap (one of its two results is the other half's word).  All but j = 16 are
+// VALU instructions, so a compare-exchange stage waits on no LDS round trip.
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v, int j) {
+    const int lane = lane_id();
+    switch (j) {
+        case 1: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+        case 2: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+        case 4: {
+            const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xF, 0xF, false);  // row_shl:4
+            const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+            return (lane & 4) ? dn : up;
+        }
+        case 8: {
+            const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x108, 0xF, 0xF, false);  // row_shl:8
+            const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+            return (lane & 8) ? dn : up;
+        }
+        case 16: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (16 << 10) | 0x1F);  // xor_mask 16, and_mask 31
+        default: {
+            const auto sw = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+            return (lane & 32) ? sw[0] : sw[1];
+        }
+    }
+}
+__device__ __forceinline__ u64 lane_xor64(u64 v, int j) {
+    return ((u64)lane_xor((uint32_t)(v >> 32), j) << 32) | (u64)lane_xor((uint32_t)v, j);
+}
+
 // compare-exchange with lane ^ j; keep the smaller key if keep_min
 __device__ __forceinline__ u64 cx(u64 v, int j, bool keep_min) {
-    u64 o = __shfl_xor(v, j);
+    const u64 o = lane_xor64(v, j);
     return keep_min ? umin64(v, o) : umax64(v, o);
 }
 
@@ -69,6 +101,34 @@ __device__ __forceinline__ void topk_merge(u64 (&T)[R], u64 x) {
         T[0] = merge64(y, true);
     } else {
         // [T0..T(R-2) ascending, T(R-1) descending] is bitonic over 64R elements
+        T[R - 1] = merge64(y, false);
+#pragma unroll
+        for (int s = R / 2; s >= 1; s >>= 1) {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                if ((r & s) == 0) {
+                    u64 a = T[r], b = T[r + s];
+                    T[r] = umin64(a, b);
+                    T[r + s] = umax64(a, b);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) T[r] = merge64(T[r], true);
+    }
+}
+
+// topk_merge for a batch that is already ascending across the lanes (a prefix of a sorted
+// list, KEY_NONE padding at the end): reversed by one lane permutation instead of sorted
+template <int R>
+__device__ __forceinline__ void topk_merge_sorted(u64 (&T)[R], u64 x) {
+    const int src = 4 * (63 - lane_id());
+    const u64 rev = ((u64)(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(x >> 32)) << 32) |
+                    (u64)(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)x);
+    u64 y = umin64(T[R - 1], rev);  // half-cleaner: the 64 smallest of T[R-1] u x, bitonic
+    if constexpr (R == 1) {
+        T[0] = merge64(y, true);
+    } else {
         T[R - 1] = merge64(y, false);
 #pragma unroll
         for (int s = R / 2; s >= 1; s >>= 1) {
@@ -137,26 +197,20 @@ __device__ __forceinline__ float u4getf(const uint4& v, int i) {
     return __uint_as_float(i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w);
 }
 
-// Wait states in front of each LDS-DMA issue (after its M0 write): the compiler's hazard
-// checks do not look inside inline asm, and a VALU write of the SGPR base the load reads
-// (v_readfirstlane) needs 5 of them before a vector-memory instruction reads it
-#ifndef KNN_DMA_NOPS
-#define KNN_DMA_NOPS "0"
-#endif
-#ifndef KNN_DMA_TAIL
-#define KNN_DMA_TAIL ""  // study: instructions after each LDS-DMA issue (e.g. "\n\ts_nop 7")
-#endif
 // LDS-DMA issued by inline asm: the compiler does not see these as LDS writes, so it
 // does not put a vmcnt(0) in front of the next LDS read (which would serialise every
 // tile's compute behind the DMA of the tile after it); the kernel orders them itself
-// with counted waits + s_barrier (wait_dma_barrier).  M0 = LDS destination (uniform).
+// with waits + s_barrier (wait_dma_barrier).  M0 = the LDS destination (wave-uniform),
+// written in the same statement that reads it (the compiler reserves M0 and does not
+// preserve it around the statement: the statement saves and restores it).  Wait states
+// inside the string, which the compiler does not pad: the SALU write of M0 needs 1 before
+// the load reads it (s_nop 0); the scalar base may come straight from v_readfirstlane (a
+// VALU write of an SGPR), which needs 5 before a vector-memory instruction reads it as its
+// base -- s_nop 2 (3) and the two M0 moves (2) open the string.  Every
+// operand is a value fixed before the statement (scalar tile base, the lane's constant
+// offset VGPR): no per-tile address arithmetic feeds a DMA.
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds) {
-    lds = __builtin_amdgcn_readfirstlane(lds);
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop " KNN_DMA_NOPS "\n\tglobal_load_lds_dwordx4 %0, off" KNN_DMA_TAIL ::"v"(gsrc), "s"(lds)
-                 : "memory", "m0");
 }
 // a wave-uniform value the compiler may have kept in VGPRs, as SGPRs
 __device__ __forceinline__ const void* sgpr_ptr(const void* p) {
@@ -169,14 +223,22 @@ __device__ __forceinline__ const void* sgpr_ptr(const void* p) {
 __device__ __forceinline__ void dma16s(uint32_t voff, const void* sbase, uint32_t lds) {
     sbase = sgpr_ptr(sbase);
     lds = __builtin_amdgcn_readfirstlane(lds);
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop " KNN_DMA_NOPS "\n\tglobal_load_lds_dwordx4 %0, %1" KNN_DMA_TAIL ::"v"(voff), "s"(sbase), "s"(lds)
-                 : "memory", "m0");
+    uint32_t keep;
+    asm volatile("s_nop 2\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(sbase), "s"(lds)
+                 : "memory");
 }
 __device__ __forceinline__ void dma4s(uint32_t voff, const void* sbase, uint32_t lds) {
     sbase = sgpr_ptr(sbase);
     lds = __builtin_amdgcn_readfirstlane(lds);
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop " KNN_DMA_NOPS "\n\tglobal_load_lds_dword %0, %1" KNN_DMA_TAIL ::"v"(voff), "s"(sbase), "s"(lds)
-                 : "memory", "m0");
+    uint32_t keep;
+    asm volatile("s_nop 2\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(sbase), "s"(lds)
+                 : "memory");
 }
 // wait until at most n (wave-uniform, <= 15) vector-memory ops of this wave are in
 // flight, then barrier: vmcnt retires in issue order for loads (the DMAs)

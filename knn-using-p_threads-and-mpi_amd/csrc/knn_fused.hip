@@ -21,40 +21,11 @@
 #include "knn_kernels.h"
 #include "knn_study.h"
 
-#ifndef KNN_FUSED_PF
-#define KNN_FUSED_PF 6  // A-fragment prefetch depth in MFMAs
-#endif
-#ifndef KNN_FUSED_DEFER
-#define KNN_FUSED_DEFER 1  // 8-wave shapes: queue passing values, flush all waves together
-#endif
-#ifndef KNN_FUSED_DEFER_EVERY
-#define KNN_FUSED_DEFER_EVERY 64  // tiles between flushes of the deferred queues
-#endif
-#ifndef KNN_FUSED_PSTEP
-#define KNN_FUSED_PSTEP 0  // 1 (study): the in-step pass set for d >= 128
-#endif
-#ifndef KNN_FUSED_PRIO
-#define KNN_FUSED_PRIO 0  // 1 (study): s_setprio 1 for the second half of the waves
-#endif
-#ifndef KNN_FUSED_LATE_DMA
-#define KNN_FUSED_LATE_DMA 0
-#endif
-#ifndef KNN_FUSED_DMA_OFS
-#define KNN_FUSED_DMA_OFS 0  // k-steps the tile's DMA pieces are shifted by within the step (study)
-#endif
-#ifndef KNN_FUSED_SHARE_EVERY
-#define KNN_FUSED_SHARE_EVERY 64  // tiles between threshold exchanges of a query's pieces (gthr)
-#endif
-#ifndef KNN_FUSED_GROUP_SET
-#define KNN_FUSED_GROUP_SET 1  // the lazy pass set by groups of 4 values first (B 703 -> 674 ms, A same)
-#endif
-#ifndef KNN_FUSED_ROW_NORM
-#define KNN_FUSED_ROW_NORM 0  // 1: the slow path's bounds use each row's norm (an LDS ring filled by DMA)
-#endif
-#ifndef KNN_FUSED_RQ
-#define KNN_FUSED_RQ 4  // deferred-queue depth per lane
-#endif
-
+// Constants of the filter (each measured against its alternatives; DESIGN.md "Filter studies")
+static constexpr int FUSED_PF = 6;            // A-fragment prefetch depth, in MFMAs
+static constexpr int FUSED_DEFER_EVERY = 64;  // 8-wave heap shapes: tiles between flushes of the queued values
+static constexpr int FUSED_SHARE_EVERY = 64;  // tiles between threshold exchanges of a query's pieces (gthr)
+static constexpr int FUSED_RQ = 4;            // queued passing values per lane (heap shapes)
 
 // ---------------------------------------------------------------------------------
 // k_aug_rows<E>: rows of the fused filter, [n][d + 16] bf16.  Element c < d is
@@ -65,8 +36,8 @@
 // 8-byte bf16 quad out.
 // ---------------------------------------------------------------------------------
 template <typename E>
-__global__ __launch_bounds__(256) void k_aug_rows(const E* __restrict__ x, int64_t n, int ld, int d,
-                                                  const float* __restrict__ norms, float scale,
+__global__ __launch_bounds__(256) void k_aug_rows(const E* __restrict__ x, int64_t n, int64_t n_valid, int ld,
+                                                  int d, const float* __restrict__ norms, float scale,
                                                   bf16_t* __restrict__ out, const int32_t* __restrict__ gate) {
     if (gate && *gate == 0) return;
     const int per_row = (d + 16) >> 2;
@@ -75,7 +46,11 @@ __global__ __launch_bounds__(256) void k_aug_rows(const E* __restrict__ x, int64
     const int64_t r = i / per_row;
     const int c = (int)(i - r * per_row) * 4;
     uint32_t w0 = 0u, w1 = 0u;
-    if (c < d) {
+    if (r >= n_valid) {
+        // pad rows up to the 64-row tile grid (train only): zero features and tn_hi = 0x1.fep127,
+        // so y = tn - 2 q.t ~ 1.7e38 never passes a fast test; their indices are past row_end
+        if (c == d && norms) w0 = 0x7f7fu;
+    } else if (c < d) {
         const float4 v = load4(x + r * ld + c);
         w0 = bf16_rne(scale * v.x) | (bf16_rne(scale * v.y) << 16);
         w1 = bf16_rne(scale * v.z) | (bf16_rne(scale * v.w) << 16);
@@ -96,17 +71,17 @@ __global__ __launch_bounds__(256) void k_aug_rows(const E* __restrict__ x, int64
     *reinterpret_cast<uint2*>(out + r * (int64_t)(d + 16) + c) = make_uint2(w0, w1);
 }
 
-hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int ld, int d, const float* norms, float scale,
-                               uint16_t* out, hipStream_t st, const int32_t* gate) {
+hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int64_t n_valid, int ld, int d, const float* norms,
+                               float scale, uint16_t* out, hipStream_t st, const int32_t* gate) {
     const int64_t total = n * ((d + 16) / 4);
     if (total <= 0) return hipSuccess;
     if (d % 4 || ld % 4) return hipErrorInvalidValue;
     const dim3 grid((unsigned)((total + 255) / 256));
     if (elem == ELEM_BF16)
-        hipLaunchKernelGGL(k_aug_rows<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, n, ld, d, norms, scale,
+        hipLaunchKernelGGL(k_aug_rows<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, n, n_valid, ld, d, norms, scale,
                            (bf16_t*)out, gate);
     else
-        hipLaunchKernelGGL(k_aug_rows<float>, grid, dim3(256), 0, st, (const float*)x, n, ld, d, norms, scale,
+        hipLaunchKernelGGL(k_aug_rows<float>, grid, dim3(256), 0, st, (const float*)x, n, n_valid, ld, d, norms, scale,
                            (bf16_t*)out, gate);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
@@ -134,7 +109,7 @@ hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int ld, int d
 // ---------------------------------------------------------------------------------
 // fused_piece: one piece of work -- query tile qt against train rows [row_begin, row_end),
 // piece (segment) id seg of that query tile (its candidate sub-slices, 2 seg + h)
-template <int RB, int NBUF, int NW, int RG, bool PSTEP, int KR>
+template <int RB, int NBUF, int NW, int RG, int KR>
 __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int qt, const int seg,
                                             const int64_t row_begin, const int64_t row_end) {
     typedef FilterTile<RB, NW, 1, RG> FT;
@@ -144,13 +119,10 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     constexpr int DMA_PER_WAVE = (DMA_INS + NW - 1) / NW;
     constexpr int NS = RB / 32;                  // k-steps: d/16 feature steps + the norm step
     constexpr int VPS = (16 + NS - 1) / NS;      // fast-test values per k-step per accumulator
-    constexpr int NR = NBUF + 1;                 // norm ring slots: tiles it-1 .. it+NBUF-1
-    constexpr int RS = BN;                       // ring slot: BN row norms
-    static_assert(NBUF == 2 || NBUF == 3 || NBUF == 4 || NBUF == 6, "tile buffers");
-    // NBUF = 2 GRP (4, 6): tiles go in groups of GRP -- one barrier per group; the DMA of tile
-    // it + GRP is issued during step it into the buffer tile it - GRP used (read before this
-    // group's barrier)
-    constexpr int GRP = (NBUF == 4 || NBUF == 6) ? NBUF / 2 : 1;
+    static_assert(NBUF == 2 || NBUF == 4, "tile buffers: two, or four (tiles in pairs)");
+    // NBUF = 4: tiles go in pairs -- one barrier per pair; the DMA of tile it + 2 is issued
+    // during step it into the buffer tile it - 2 used (read before this pair's barrier)
+    constexpr int GRP = NBUF == 4 ? 2 : 1;
     constexpr bool PAIR = GRP > 1;
     constexpr int AHEAD = PAIR ? GRP : NBUF - 1;  // tiles between a step and the tile it DMAs
     static_assert(RG == 1 || RG == 2, "row groups");
@@ -160,16 +132,14 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     constexpr int LL = 16;             // register list length
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* tiles = smem;                                     // [NBUF][TILE]
-    float* ring = reinterpret_cast<float*>(smem + NBUF * TILE);      // [NR][RS] train norms tn
     const int hs = heap_stride(a.k);
-    float* topU = ring + NR * RS;                                    // [BM][hs] max-heaps of U
+    float* topU = reinterpret_cast<float*>(smem + NBUF * TILE);      // [BM][hs] max-heaps of U
     const int cap_sub = a.cap_seg / 2;  // candidate sub-slice of one lane half (h) of a query
 
     const int lane = lane_id();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int j = lane & 31;
     const int h = lane >> 5;
-    if (KNN_FUSED_PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
     const int k = a.k;
     const float INF = __uint_as_float(0x7f800000u);
     const float coef = a.coef, eta = a.eta;
@@ -182,7 +152,6 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             topU[i] = (e == hs - 1 || e <= k - 2) ? INF : -INF;  // root, nodes 1..k-1: +inf
         }
     }
-    for (int i = threadIdx.x; i < NR * RS; i += NT) ring[i] = INF;
 
     // this lane's query (both lane halves hold the same query, different rows)
     const int jl = wave * 32 + j;
@@ -232,7 +201,10 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     const int ntiles = (row_end > row_begin) ? (int)((row_end - row_begin + BN - 1) / BN) : 0;
 
     // ---- LDS-DMA of tiles (same image as k_gemm_filter: slot P -> row P / SLOTS, slot P % SLOTS,
-    // the pad slot duplicates slot 0; rows past nt read row nt-1 and are rejected by index)
+    // the pad slot duplicates slot 0; rows past row_end are read (padding or the next piece's
+    // rows) and rejected by index).  Every tile is whole: the augmented train rows are padded to
+    // the 64-row grid (run_gemm), so a piece is always the scalar tile base + this lane's fixed
+    // offset -- no per-tile address arithmetic in VGPRs.
     uint32_t doff[DMA_PER_WAVE];
 #pragma unroll
     for (int i = 0; i < DMA_PER_WAVE; i++) {
@@ -240,55 +212,30 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         const int row = min(P / SLOTS, BN - 1), sl = P % SLOTS;
         doff[i] = (uint32_t)(row * ldb + 16 * (sl == SLOTS - 1 ? 0 : sl));
     }
-    // this wave's vector-memory ops per tile: its DMA pieces (+ the norm ring load of the
-    // last wave) and the tile-max load
-    int n_dma_wave = (KNN_FUSED_ROW_NORM && wave == NW - 1) ? 2 : 1;
-#pragma unroll
-    for (int i = 0; i < DMA_PER_WAVE; i++) n_dma_wave += (wave + NW * i < DMA_INS) ? 1 : 0;
-    constexpr int NPIECE = DMA_PER_WAVE + (KNN_FUSED_ROW_NORM ? 1 : 0);
     const uint32_t lds_tiles = __builtin_amdgcn_readfirstlane(lds_addr(tiles));
-    const uint32_t lds_ring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
-    struct DmaTile { const unsigned char* src; uint32_t lds, lring; int64_t r0; bool full; };
-    auto dma_desc = [&](int buf, int slot, int64_t r0) -> DmaTile {
-        return DmaTile{trainb + r0 * ldb, lds_tiles + (uint32_t)(buf * TILE), lds_ring + (uint32_t)(slot * RS * 4), r0,
-                       r0 + BN <= a.nt};
+    struct DmaTile { const unsigned char* src; uint32_t lds; };
+    auto dma_desc = [&](int buf, int64_t r0) -> DmaTile {
+        return DmaTile{trainb + r0 * ldb, lds_tiles + (uint32_t)(buf * TILE)};
     };
     auto dma_piece = [&](int i, const DmaTile& d) __attribute__((always_inline)) {
-        if (i < DMA_PER_WAVE) {
-            const int ins = wave + NW * i;
-            if (ins < DMA_INS) {
-                if (i == DMA_PER_WAVE - 1 && ins == DMA_INS - 1 && lane >= FT::LAST_LANES) return;
-                const uint32_t dst = d.lds + (uint32_t)ins * 1024u;
-                if (d.full) {
-                    dma16s(doff[i], d.src, dst);
-                } else {
-                    const int P = ins * 64 + lane;
-                    const int row = P / SLOTS, sl = P % SLOTS;
-                    const int64_t t = min(d.r0 + row, a.nt - 1);
-                    dma16(trainb + t * ldb + 16 * (sl == SLOTS - 1 ? 0 : sl), dst);
-                }
-            }
-        } else if (wave == NW - 1 && lane < BN) {
-            dma4s(4u * lane, a.tnorm + d.r0, d.lring);
+        const int ins = wave + NW * i;
+        if (ins < DMA_INS) {
+            if (i == DMA_PER_WAVE - 1 && ins == DMA_INS - 1 && lane >= FT::LAST_LANES) return;
+            dma16s(doff[i], d.src, d.lds + (uint32_t)ins * 1024u);
         }
     };
-    auto dma_tile = [&](int buf, int slot, int64_t r0) __attribute__((always_inline)) {
-        const DmaTile d = dma_desc(buf, slot, r0);
-#pragma unroll
-        for (int i = 0; i < NPIECE; i++) dma_piece(i, d);
-    };
+    // piece i goes out in k-step (i NS) / DMA_PER_WAVE of the step
     auto dma_at = [&](int s, bool on, const DmaTile& d) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < NPIECE; i++)
-            if (on && ((i * NS) / NPIECE + KNN_FUSED_DMA_OFS) % NS == s) dma_piece(i, d);
+        for (int i = 0; i < DMA_PER_WAVE; i++)
+            if (on && (i * NS) / DMA_PER_WAVE == s) dma_piece(i, d);
     };
 
-    // ---- one tile's MFMAs into X; in between, the fast test of the previous tile (Y): bit
-    // 16c + r of the returned set is 1 iff value r of accumulator c passes (y <= tf) in some
-    // lane (one v_cmp per value into an SGPR pair; the scalar ops issue beside the MFMAs --
-    // measured faster on A than a v_min3 chain plus a separate pass over the values)
-    constexpr int PF = KNN_FUSED_PF / NACC;  // k-steps of A fragments read ahead
-    uint4 pa[PF], pb[PF];                    // PAIR: the odd step's first fragments, read early
+    // ---- one tile's MFMAs into X; in between, the fast test of the previous tile (Y): a v_min3
+    // chain per accumulator; returns bit 16c (x 0xffff) when some lane of accumulator c holds a
+    // passing value (the slow path builds the value set, pass_set)
+    constexpr int PF = FUSED_PF / NACC;  // k-steps of A fragments read ahead
+    uint4 pa[PF], pb[PF];                // PAIR: the odd step's first fragments, read early
     auto prefetch = [&](int buf) __attribute__((always_inline)) {
         const unsigned char* tile = tiles + buf * TILE;
         const unsigned char* a0p = tile + j * STRIDE + 16 * h;
@@ -304,10 +251,8 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         const unsigned char* tile = tiles + buf * TILE;
         const unsigned char* a0p = tile + j * STRIDE + 16 * h;
         const unsigned char* a1p = tile + ((RG == 2 ? 32 : 0) + j) * STRIDE + 16 * h;
-        KNN_STUDY_STEP_HEAD();
 #pragma unroll
         for (int c = 0; c < NACC; c++) X[c] = floatx16{};
-        uint32_t u = 0u;
         float mn[NACC];
 #pragma unroll
         for (int c = 0; c < NACC; c++) mn[c] = INF;
@@ -333,36 +278,20 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             for (int c = 0; c < NACC; c++) {
                 const bf16x8 A = __builtin_bit_cast(bf16x8, (RG == 2 && c) ? xb[s] : xa[s]);
                 X[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, __builtin_bit_cast(bf16x8, qf[s]), X[c], 0, 0, 0);
-#ifndef KNN_ABLATE_NO_EPI
-                if constexpr (PSTEP) {
-#pragma unroll
-                    for (int v = s * VPS; v < (s + 1) * VPS && v < 16; v++)
-                        u |= (__ballot(Y[c][v] <= tf) != 0ull ? 1u : 0u) << (16 * c + v);
-                } else {
+                if (!KNN_STUDY_NO_EPI) {
 #pragma unroll
                     for (int v = s * VPS; v < (s + 1) * VPS && v < 16; v++) mn[c] = fminf(mn[c], Y[c][v]);
                 }
-#endif
             }
-            // keep this k-step's order (prefetch, MFMA, VALU): load-bearing -- relaxed, the
-            // filter runs 11 % faster and drops true neighbours (DESIGN.md "Next" 1)
-            KNN_STUDY_KSTEP_BARRIER(s);
+            KNN_FUSED_KSTEP_ORDER();
         }
-        if constexpr (!PSTEP) {
-            // which accumulators hold a passing value; the slow path builds their value sets
-            // (pass_set) -- usually one of the two
+        // which accumulators hold a passing value; the slow path builds their value sets
+        // (pass_set) -- usually one of the two
+        uint32_t u = 0u;
 #pragma unroll
-            for (int c = 0; c < NACC; c++) u |= __ballot(mn[c] <= tf) != 0ull ? (0xffffu << (16 * c)) : 0u;
-        }
+        for (int c = 0; c < NACC; c++) u |= __ballot(mn[c] <= tf) != 0ull ? (0xffffu << (16 * c)) : 0u;
         return u;
     };
-
-#ifdef KNN_FILTER_TIMING
-    unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define KNN_TSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#else
-#define KNN_TSTAMP(v)
-#endif
 
     // append candidate (L, U) of global row t to this lane half's sub-slice (past its
     // capacity: counted only, the rescore then sends the query to the exact scan)
@@ -416,14 +345,12 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             make_tfb();
         }
     };
-    // certified bounds L <= D <= U of value y of row `row` of tile tp: Delta = coef (qn + tn)
-    // + eta with tn the row's norm (KNN_FUSED_ROW_NORM, from the ring) or, by default, the
-    // tile's maximum norm tm >= tn -- a slightly wider band (still L <= D <= U), and no LDS
-    // read and wait per visited value
-    auto bounds = [&](float y, int row, int tp, float2 tq, float& L, float& U) __attribute__((always_inline)) {
+    // certified bounds L <= D <= U of value y against tile stats tq: Delta = coef (qn + tmax)
+    // + eta + rho -- the tile's maximum norm tmax >= the row's norm, a slightly wider band
+    // (still L <= D <= U) for no per-value norm read
+    auto bounds = [&](float y, float2 tq, float& L, float& U) __attribute__((always_inline)) {
         const float G = qn + y;
-        const float tn = KNN_FUSED_ROW_NORM ? ring[(tp % NR) * RS + row] : tq.x;
-        const float dl = fmaf(coef, qn + tn, eta) + tq.y;
+        const float dl = fmaf(coef, qn + tq.x, eta) + tq.y;
         L = G - dl;
         U = G + dl;
     };
@@ -436,18 +363,14 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         if constexpr (NACC == 1) return Y[0][v & 15];
         else return (v >> 4) ? Y[1][v & 15] : Y[0][v & 15];
     };
-    // the values of Y some lane passes (bit 16c + r): one v_cmp per value into an SGPR pair,
-    // then scalar ops (the !PSTEP variant builds it only on tiles some value passes).
-    // Measured (same box): sets by groups of 4 values (a min of 4 per ballot) are slower on A
-    // and B -- the extra slow-path visits cost more than the scalar ops they save.
-    auto pass_set = [&](floatx16 (&Y)[NACC], float tf, uint32_t acc = 0xffffffffu) __attribute__((always_inline)) -> uint32_t {
+    // the values of Y some lane passes (bit 16c + r), for the accumulators set in acc: per
+    // group of 4 values (rows 8g .. 8g+3 of the lane half) one ballot of their minimum, then
+    // one v_cmp + ballot per value of the passing groups only
+    auto pass_set = [&](floatx16 (&Y)[NACC], float tf, uint32_t acc) __attribute__((always_inline)) -> uint32_t {
         uint32_t u = 0u;
 #pragma unroll
         for (int c = 0; c < NACC; c++)
             if ((acc >> (16 * c)) & 1u) {  // (wave-uniform) only the accumulators that pass
-#if KNN_FUSED_GROUP_SET
-                // then only the groups of 4 values (rows 8g .. 8g+3 of the lane half) whose
-                // minimum passes
 #pragma unroll
                 for (int g = 0; g < 4; g++) {
                     const float gm = fminf(fminf(Y[c][4 * g], Y[c][4 * g + 1]), fminf(Y[c][4 * g + 2], Y[c][4 * g + 3]));
@@ -457,18 +380,14 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                             u |= (__ballot(Y[c][r] <= tf) != 0ull ? 1u : 0u) << (16 * c + r);
                     }
                 }
-#else
-#pragma unroll
-                for (int r = 0; r < 16; r++) u |= (__ballot(Y[c][r] <= tf) != 0ull ? 1u : 0u) << (16 * c + r);
-#endif
             }
         return u;
     };
-    // immediate slow path: the passing values of tile tp, visited by index; the two lanes
-    // of a query take turns (one heap writer at a time)
+    // immediate slow path (4-wave heap shapes): the passing values of tile tp, visited by
+    // index; the two lanes of a query take turns (one heap writer at a time)
     auto slow = [&](floatx16 (&Y)[NACC], int tp, float tf, float2 tq, uint32_t u) {
         const int64_t tbase = row_begin + (int64_t)tp * BN;
-        if constexpr (!PSTEP) u = pass_set(Y, tf, u);
+        u = pass_set(Y, tf, u);
         while (u) {
             const int v = __builtin_ctz(u);
             u &= u - 1u;
@@ -482,7 +401,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                 if (!__ballot(p && h == hh)) continue;
                 if (p && h == hh && t < row_end) {
                     float L, U;
-                    bounds(y, row, tp, tq, L, U);
+                    bounds(y, tq, L, U);
                     accept(L, U, t);
                 }
                 sync_roots(hh);
@@ -513,17 +432,15 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         for (int i = LL - 1; i >= 1; i--) lst[i] = __builtin_amdgcn_fmed3f(lst[i - 1], w, lst[i]);
         lst[0] = fminf(lst[0], w);
     };
-    // the other lane half's copy of a word (v_permlane32_swap: one result of the swap is this
-    // lane's own word, the other its partner's)
+    // the other lane half's copy of a word (v_permlane32_swap: one of the swap's two results
+    // is this lane's own word, the other its partner's)
     auto partner = [&](float x) __attribute__((always_inline)) -> float {
-        const uint32_t xb = __float_as_uint(x);
-        const auto sw = __builtin_amdgcn_permlane32_swap(xb, xb, false, false);
-        return __uint_as_float(sw[0] == xb ? sw[1] : sw[0]);
+        return __uint_as_float(lane_xor(__float_as_uint(x), 32));
     };
     auto slow_rl = [&](floatx16 (&Y)[NACC], int tp, float tf, float2 tq, uint32_t u) {
         if constexpr (RL) {
             const int64_t tbase = row_begin + (int64_t)tp * BN;
-            if constexpr (!PSTEP) u = pass_set(Y, tf, u);
+            u = pass_set(Y, tf, u);
             while (u) {
                 const int v = __builtin_ctz(u);
                 u &= u - 1u;
@@ -532,7 +449,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                 const int row = 32 * (v >> 4) + (r & 3) + 8 * (r >> 2) + 4 * h;
                 const int64_t t = tbase + row;
                 float L, U;
-                bounds(y, row, tp, tq, L, U);
+                bounds(y, tq, L, U);
                 const bool keep = y <= tf && t < row_end && L <= thr;
                 if (keep) store_cand(L, U, t);
                 const float w = (keep && U < lst[LL - 1]) ? U : INF;
@@ -555,24 +472,19 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         }
     };
 
-    // deferred slow path (8-wave shapes): passing values with L <= thr are queued -- (L, U,
-    // row) in registers -- and flushed through accept() every DEFER_EVERY tiles by all waves
-    // together, or when some lane's queue is full.  A threshold waiting for the flush is
-    // stale but still valid (it only ever tightens).
-    // the queue is three register vectors read with a wave-uniform index (v_movrels), so
-    // the flush is a runtime loop with one copy of accept()
-    bool dirty = false;  // this wave issued vector-memory ops after the newest DMA
-    constexpr int RQ = KNN_FUSED_RQ;
-    static_assert(RQ == 2 || RQ == 4 || RQ == 8, "queue depth");
+    // deferred slow path (8-wave heap shapes): passing values with L <= thr are queued -- (L,
+    // U, row) in registers -- and flushed through accept() every FUSED_DEFER_EVERY tiles by all
+    // waves together, or when some lane's queue is full.  A threshold waiting for the flush is
+    // stale but still valid (it only ever tightens).  The queue is three register vectors read
+    // with a wave-uniform index (v_movrels), so the flush is a runtime loop with one copy of
+    // accept()
+    constexpr int RQ = FUSED_RQ;
     typedef float qvecf __attribute__((ext_vector_type(RQ)));
     typedef int qveci __attribute__((ext_vector_type(RQ)));
     qvecf qL = qvecf{}, qU = qvecf{};
     qveci qT = qveci{};
     int qcnt = 0;
     auto flush = [&]() __attribute__((always_inline)) {
-#ifdef KNN_FILTER_TIMING
-        const unsigned long long tf0 = __builtin_amdgcn_s_memtime();
-#endif
 #pragma unroll 1
         for (int hh = 0; hh < 2; hh++) {
 #pragma unroll 1
@@ -585,18 +497,10 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         }
         qcnt = 0;
         publish();
-#ifdef KNN_FILTER_TIMING
-        tph[6] += 1;
-        tph[7] += __builtin_amdgcn_s_memtime() - tf0;
-#endif
     };
     auto record = [&](floatx16 (&Y)[NACC], int tp, float tf, float2 tq, uint32_t u) {
         const int64_t tbase = row_begin + (int64_t)tp * BN;
-        if constexpr (!PSTEP) u = pass_set(Y, tf, u);
-#ifdef KNN_FILTER_TIMING
-        tph[4] += 1;
-        tph[5] += __builtin_popcount(u);
-#endif
+        u = pass_set(Y, tf, u);
         while (u) {
             const int v = __builtin_ctz(u);
             u &= u - 1u;
@@ -608,7 +512,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             const int64_t t = tbase + row;
             if (p && t < row_end) {
                 float L, U;
-                bounds(y, row, tp, tq, L, U);
+                bounds(y, tq, L, U);
                 if (L <= thr) {
 #pragma unroll
                     for (int i = 0; i < RQ; i++) {
@@ -628,20 +532,18 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     __syncthreads();  // LDS init is complete before any DMA lands
 #pragma unroll
     for (int p = 0; p < AHEAD; p++)
-        if (p < ntiles) dma_tile(p, p, row_begin + (int64_t)p * BN);
-#ifndef KNN_FUSED_EARLY_DMA
-#define KNN_FUSED_EARLY_DMA 0
-#endif
-    // KNN_FUSED_LATE_DMA (study): tiles in groups also issue their DMA after the step
-    constexpr bool LATE_DMA = (NBUF == 3 && !KNN_FUSED_EARLY_DMA) || (NBUF >= 4 && KNN_FUSED_LATE_DMA);
-    constexpr bool DEFER = NW == 8 && KNN_FUSED_DEFER && !RL;
-    constexpr int DEFER_EVERY = KNN_FUSED_DEFER_EVERY;
-    // per-64-row maximum train norm of the tile in the pipeline (tile it) and of tile it-1
+        if (p < ntiles) {
+            const DmaTile d0 = dma_desc(p, row_begin + (int64_t)p * BN);
+#pragma unroll
+            for (int i = 0; i < DMA_PER_WAVE; i++) dma_piece(i, d0);
+        }
+    constexpr bool DEFER = NW == 8 && !RL;
+    // tile terms (max norm, rounding bound) of the tile in the pipeline (it) and of tile it-1
     const int64_t tile0 = row_begin >> 6;
     float2 tm_prev = make_float2(0.0f, 0.0f);
-    float2 tmg[GRP];  // PAIR: the group's tile terms, loaded after its barrier
+    float2 tmg[GRP];  // PAIR: the pair's tile terms, loaded after its barrier
     auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
-        if ((it & (KNN_FUSED_SHARE_EVERY - 1)) == KNN_FUSED_SHARE_EVERY - 1) {
+        if ((it & (FUSED_SHARE_EVERY - 1)) == FUSED_SHARE_EVERY - 1) {
             if (a.nseg > 1 && qvalid) {
                 if constexpr (RL) {  // publish this query's bound (the heap path does it per accept)
                     if (h == 0 && thr < published) {
@@ -654,22 +556,13 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                 if (gv < thr) { thr = gv; make_tfb(); }
             }
         }
-        KNN_TSTAMP(t0);
-        if constexpr (PAIR) {
-            // pair (it, it + 1) starts: both tiles have landed (every wave's pieces), and
-            // every wave is done with the previous pair's buffers
-            if (it % GRP == 0) wait_dma_barrier(0);
-        } else {
-            const bool keep_next = NBUF == 3 && it + 1 < ntiles && (LATE_DMA || !dirty);
-            wait_dma_barrier(keep_next ? n_dma_wave : 0);
-        }
-        dirty = false;
-        // this tile's maximum train norm, for its fast test in the next iteration: issued after
-        // the barrier, it lands under this step (the next barrier's wait covers it)
+        // the tiles of this step (both of a pair) have landed -- every wave's pieces: each wave
+        // waits for all of its own vector-memory ops, then the barrier -- and every wave is done
+        // with the buffers the next DMAs overwrite
+        if (!PAIR || it % GRP == 0) wait_dma_barrier(0);
+        // this tile's terms, for its fast test in the next iteration: loaded after the barrier
         float2 tm_cur;
         if constexpr (PAIR) {
-            // both tiles' maxima after the pair's barrier: no compiler wait on a load issued
-            // before the DMA of the second step (it would wait for that DMA too)
             const int gi = it % GRP;
             if (gi == 0) {
 #pragma unroll
@@ -681,45 +574,26 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         } else {
             tm_cur = tile_q(tile0 + ((it * BN) >> 6));
         }
-        KNN_TSTAMP(t1);
-#ifndef KNN_ABLATE_NO_DMA
-        const bool dma_on = it + AHEAD < ntiles;
-#else
-        const bool dma_on = false;
-#endif
-        const DmaTile dd = dma_desc((it + AHEAD) % NBUF, (it + AHEAD) % NR, row_begin + (int64_t)(it + AHEAD) * BN);
+        const bool dma_on = !KNN_STUDY_NO_DMA && it + AHEAD < ntiles;
+        const DmaTile dd = dma_desc((it + AHEAD) % NBUF, row_begin + (int64_t)(it + AHEAD) * BN);
         const float tf = it > 0 ? tf_of(tm_prev) : -INF;
-        // (measured slower: both tiles of the next pair DMA'd in one burst after the even step,
-        // A 28.0 -> 28.5 ms, B 752 -> 802 ms)
-        const uint32_t uY = step(X, Y, it % NBUF, dma_on && !LATE_DMA, dd, tf, PAIR && it % GRP != 0);
-        // PAIR: the group's next tile is resident since its barrier -- its first fragments
-        // are read now, so their latency hides under the slow path below
+        const uint32_t uY = step(X, Y, it % NBUF, dma_on, dd, tf, PAIR && it % GRP != 0);
+        // PAIR: the pair's next tile is resident since its barrier -- its first fragments are
+        // read now, so their latency hides under the slow path below
         if (PAIR && it % GRP != GRP - 1 && it + 1 < ntiles) prefetch((it + 1) % NBUF);
-        KNN_TSTAMP(t2);
-#ifndef KNN_ABLATE_NO_SLOW
-        if (uY) {
-            if constexpr (RL) { slow_rl(Y, it - 1, tf, tm_prev, uY); dirty = true; }
-            else if constexpr (DEFER) record(Y, it - 1, tf, tm_prev, uY);
-            else { slow(Y, it - 1, tf, tm_prev, uY); dirty = true; }
-        }
-        if constexpr (DEFER) {
-            if ((it & (DEFER_EVERY - 1)) == DEFER_EVERY - 1 && __ballot(qcnt > 0)) {
-                flush();
-                dirty = true;
+        if (!KNN_STUDY_NO_SLOW) {
+            if (uY) {
+                if constexpr (RL) slow_rl(Y, it - 1, tf, tm_prev, uY);
+                else if constexpr (DEFER) record(Y, it - 1, tf, tm_prev, uY);
+                else slow(Y, it - 1, tf, tm_prev, uY);
             }
-        }
-#else
-        asm volatile("" ::"s"(uY));
-#endif
-        if (LATE_DMA && dma_on) {
-#pragma unroll
-            for (int i = 0; i < NPIECE; i++) dma_piece(i, dd);
+            if constexpr (DEFER) {
+                if ((it & (FUSED_DEFER_EVERY - 1)) == FUSED_DEFER_EVERY - 1 && __ballot(qcnt > 0)) flush();
+            }
+        } else {
+            asm volatile("" ::"s"(uY));
         }
         tm_prev = tm_cur;
-#ifdef KNN_FILTER_TIMING
-        KNN_TSTAMP(t3);
-        tph[0] += t1 - t0; tph[2] += t2 - t1; tph[3] += t3 - t2;
-#endif
     };
     for (int it = 0; it < ntiles; it += 2) {
         iter(accA, accB, it);
@@ -729,14 +603,11 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         // drain: the last tile's accumulators are in accA (ntiles odd) or accB (even)
         const int last = ntiles - 1;
         auto drain = [&](floatx16 (&Lc)[NACC]) {
-            KNN_STUDY_STEP_HEAD();
             const float tf = tf_of(tm_prev);
-            uint32_t u = pass_set(Lc, tf);
-            if (u) {
-                if constexpr (!PSTEP) u = 0xffffffffu;  // the slow paths rebuild the set per accumulator
-                if constexpr (RL) slow_rl(Lc, last, tf, tm_prev, u);
-                else if constexpr (DEFER) record(Lc, last, tf, tm_prev, u);
-                else slow(Lc, last, tf, tm_prev, u);
+            if (pass_set(Lc, tf, 0xffffffffu)) {
+                if constexpr (RL) slow_rl(Lc, last, tf, tm_prev, 0xffffffffu);
+                else if constexpr (DEFER) record(Lc, last, tf, tm_prev, 0xffffffffu);
+                else slow(Lc, last, tf, tm_prev, 0xffffffffu);
             }
         };
         if (last & 1) drain(accB);
@@ -751,19 +622,6 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
     if (qvalid) a.cnt[(int64_t)(2 * seg + h) * a.nq + q] = ccnt;
-#ifdef KNN_FILTER_TIMING
-    if (a.timing && lane == 0) {
-        atomicAdd(&a.timing[0], tph[0]);
-        atomicAdd(&a.timing[2], tph[2]);
-        atomicAdd(&a.timing[3], tph[3]);
-        atomicAdd(&a.timing[4], 1ull);
-        atomicAdd(&a.timing[6], tph[4]);  // record calls
-        atomicAdd(&a.timing[7], tph[5]);  // passing value indices visited
-        atomicAdd(&a.timing[8], tph[6]);  // flushes
-        atomicAdd(&a.timing[5], tph[7]);  // flush clocks
-    }
-#endif
-#undef KNN_TSTAMP
 }
 
 // The grid (knn_fused_schedule): blocks [0, p1) take one whole query tile each (qt = block,
@@ -774,7 +632,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
 // last round of blocks ends together instead of a partial wave of whole query tiles.
 // Pieces of one query tile share thresholds through gthr like segments (piece id = block -
 // the first block of that query tile).  One call site of fused_piece (instruction cache).
-template <int RB, int MINW, int NBUF, int NW, int RG, bool PSTEP, int KR>
+template <int RB, int MINW, int NBUF, int NW, int RG, int KR>
 __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) {
     if ((a.gate && *a.gate == 0) || (*a.status & KNN_STATUS_GEMM_UNSAFE)) return;  // not taken / exact path
     const int64_t T = a.tiles64;  // 64-row units per query tile
@@ -810,7 +668,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
             adv = t1 - t0;
         }
         if (!first) __syncthreads();  // every wave is done with the previous piece's LDS
-        fused_piece<RB, NBUF, NW, RG, PSTEP, KR>(a, qt, seg, rb, re);
+        fused_piece<RB, NBUF, NW, RG, KR>(a, qt, seg, rb, re);
         x += adv;
     }
 }
@@ -846,84 +704,69 @@ int knn_fused_schedule(GemmFilterArgs& a, int slots, int* nseg) {
 static size_t fused_lds_of(int row_bytes, int k, int nw, int rg, int nbuf, bool heaps) {
     const int bn = 32 * rg, bm = 32 * nw;
     const int ins = (bn * (row_bytes / 16 + 1) + 63) / 64;
-    return (size_t)nbuf * ins * 1024 + ((size_t)(nbuf + 1) * bn + (heaps ? (size_t)bm * heap_stride(k) : 0)) * sizeof(float);
+    return (size_t)nbuf * ins * 1024 + (heaps ? (size_t)bm * heap_stride(k) * sizeof(float) : 0);
 }
 
 bool knn_fused_supported(int d) { return d == 64 || d == 128 || d == 256; }
 
-// Shapes (d = features; rows of 2d + 32 bytes):
-//  d = 64:   4 waves x 32 queries, 64-row tiles, two blocks per CU (short rows: the per-tile
-//            barrier and fast test outweigh 5 MFMAs per 32x32 block; the other block hides them)
-//  d >= 128: 8 waves x 32 queries (two waves per SIMD), 64-row tiles, double-buffered; 32-row
-//            tiles when the per-query heaps of a large k leave no room for 64-row tiles.
-// Thresholds: k <= 16 keeps per-query register lists (KR = 16), k <= 32 per-half lists
-// (KR = 32, 16 entries: exact 32-entry lists cost a block per CU of occupancy and 9 % of
-// time on B), larger k the LDS heaps.
-FilterPlan knn_fused_plan(int d, int k, const FilterStudy* fs) {
+// Shapes (d = features; rows of 2d + 32 bytes).  Block = NW waves x 32 queries:
+//  * k <= 32 (register lists, KR = 16 / 32): 8 waves, 64-row tiles in pairs (four buffers,
+//    one barrier per two tiles) -- measured on A: 33.4 -> 31.3 ms against two buffers; B
+//    (d = 64): 765 ms with 4-wave blocks, 743 with 8 (256 queries share a tile's DMA).
+//  * k > 32 (LDS heaps, KR = 0): d = 64 in 4-wave blocks, two buffers, two blocks per CU
+//    (the other block hides the per-tile barrier and fast test of 5-step tiles); d >= 128 in
+//    8-wave blocks: pairs when they fit beside the heaps, else two buffers, else 32-row tiles
+//    (C: d = 256, k = 100).
+// Register lists: k <= 16 keeps per-query lists (KR = 16), k <= 32 per-half lists (KR = 32,
+// 16 entries: exact 32-entry lists cost a block per CU of occupancy and 9 % of time on B).
+FilterPlan knn_fused_plan(int d, int k) {
     const int rb = 2 * d + 32;
-    const size_t cap = 160 * 1024 - 256;  // room for the kernel's static LDS (the start tile)
-    // pass-set variant (FilterPlan.qg): the v_min3 chain and a lazy pass set for every d --
-    // measured on A (same box, with the rounding certificate): 29.8 (in-step set) -> 28.8 ms
-    const int pstep = (d >= 128 && KNN_FUSED_PSTEP) ? 1 : 0;
-    int kr = k <= 16 ? 16 : k <= 32 ? 32 : 0;
-    if (fs && fs->kr == 0) kr = 0;  // study: the heaps for every k
+    const size_t cap = 160 * 1024 - 256;  // room for the kernel's static LDS
+    const int kr = k <= 16 ? 16 : k <= 32 ? 32 : 0;
     auto make = [&](int nw, int rg, int minw, int nbuf) {
-        FilterPlan f{nw, pstep, rg, minw, nbuf, 32 * nw, fused_lds_of(rb, k, nw, rg, nbuf, kr == 0)};
+        FilterPlan f{nw, 0, rg, minw, nbuf, 32 * nw, fused_lds_of(rb, k, nw, rg, nbuf, kr == 0)};
         f.kr = kr;
         return f;
     };
-    const bool force8 = fs && fs->shape[0] == 'w' && fs->shape[1] == '8';
-    // study: 3 buffers or pairs (4); triples (6) measured slower (A 28.0 -> 31.9 ms, B 749 -> 995)
-    const int nb = fs && (fs->nbuf == 3 || fs->nbuf == 4) ? fs->nbuf : 2;
-    const bool force4 = fs && fs->shape[0] == 'w' && fs->shape[1] == '4';
-    // d = 64 with register lists: 8-wave blocks in pairs like d >= 128 (B, same box: 765 ms
-    // with 4-wave blocks in pairs, 743 with 8-wave) -- 256 queries share each tile's DMA
-    if ((d == 64 || force4) && !force8 && kr == 0 && fused_lds_of(rb, k, 4, 2, nb, true) <= cap / 2) return make(4, 2, 2, nb);
-    if (force4 && fused_lds_of(rb, k, 4, 2, nb, kr == 0) <= cap / 2) return make(4, 2, 2, nb);
-    // d >= 128: tiles in pairs (one barrier per two tiles) when four buffers fit -- measured
-    // on A (same box): filter 33.4 -> 31.3 ms; B's d = 64 shape loses occupancy with them
-    const bool study_nb = fs && fs->nbuf > 0;
-    if (!study_nb && fused_lds_of(rb, k, 8, 2, 4, kr == 0) <= cap) return make(8, 2, 2, 4);
-    if (fused_lds_of(rb, k, 8, 2, nb, kr == 0) <= cap) return make(8, 2, 2, nb);
+    if (kr == 0 && d == 64 && fused_lds_of(rb, k, 4, 2, 2, true) <= cap / 2) return make(4, 2, 2, 2);
+    if (fused_lds_of(rb, k, 8, 2, 4, kr == 0) <= cap) return make(8, 2, 2, 4);
+    if (fused_lds_of(rb, k, 8, 2, 2, kr == 0) <= cap) return make(8, 2, 2, 2);
     if (fused_lds_of(rb, k, 8, 1, 2, kr == 0) <= cap) return make(8, 1, 2, 2);
     return FilterPlan{0, 0, 0, 0, 0, 0, 0};  // k too large for the LDS heaps: not supported
 }
 
-// FilterPlan.qg carries the pass-set variant of the fused kernel: 1 = built in the step
-// (PSTEP: a v_cmp per value between the MFMAs; d >= 128, where the MFMAs hide it), 0 = a
-// v_min3 chain in the step and the set built on passing tiles only (d = 64: 10 MFMAs per
-// tile leave no room).  Measured on one box: A (d = 128) PSTEP faster, B (d = 64) slower.
-template <int RB, bool P, int KR>
-static const void* fused_fn_p(const FilterPlan& f) {
-#define KNN_FUSED_FN(NB, NW, RG) reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, NB, NW, RG, P, KR>)
-    if (f.nw == 4) return f.nbuf == 4 ? KNN_FUSED_FN(4, 4, 2) : f.nbuf == 3 ? KNN_FUSED_FN(3, 4, 2) : KNN_FUSED_FN(2, 4, 2);
-    if (f.rg == 2) return f.nbuf == 4 ? KNN_FUSED_FN(4, 8, 2) : f.nbuf == 3 ? KNN_FUSED_FN(3, 8, 2) : KNN_FUSED_FN(2, 8, 2);
-    return KNN_FUSED_FN(2, 8, 1);
-#undef KNN_FUSED_FN
-}
-template <int RB, bool P>
+template <int RB, int KR>
 static const void* fused_fn_k(const FilterPlan& f) {
-    return f.kr == 16 ? fused_fn_p<RB, P, 16>(f) : f.kr == 32 ? fused_fn_p<RB, P, 32>(f) : fused_fn_p<RB, P, 0>(f);
+#define KNN_FUSED_FN(NB, NW, RG) reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, NB, NW, RG, KR>)
+    if constexpr (KR > 0) {
+        return KNN_FUSED_FN(4, 8, 2);  // register lists always fit the pairs shape
+    } else {
+        if (f.nw == 4) return KNN_FUSED_FN(2, 4, 2);
+        if (f.rg == 2) return f.nbuf == 4 ? KNN_FUSED_FN(4, 8, 2) : KNN_FUSED_FN(2, 8, 2);
+        return KNN_FUSED_FN(2, 8, 1);
+    }
+#undef KNN_FUSED_FN
 }
 template <int RB>
 static const void* fused_fn(const FilterPlan& f) {
-    return fused_fn_k<RB, (RB >= 288) && KNN_FUSED_PSTEP>(f);  // the pass-set variant (knn_fused_plan)
+    return f.kr == 16 ? fused_fn_k<RB, 16>(f) : f.kr == 32 ? fused_fn_k<RB, 32>(f) : fused_fn_k<RB, 0>(f);
 }
 
 static const void* fused_ptr(int d, const FilterPlan& f) {
     return d == 64 ? fused_fn<160>(f) : d == 128 ? fused_fn<288>(f) : fused_fn<544>(f);
 }
 
-hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu, const FilterStudy* fs) {
-    const FilterPlan f = knn_fused_plan(d, k, fs);
+hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu) {
+    const FilterPlan f = knn_fused_plan(d, k);
     if (!knn_fused_supported(d) || f.nw == 0) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fused_ptr(d, f), 64 * f.nw, f.lds);
 }
 
-hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st, const FilterStudy* fs) {
-    const FilterPlan f = knn_fused_plan(a.d, a.k, fs);
+hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st) {
+    const FilterPlan f = knn_fused_plan(a.d, a.k);
     if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != a.d + 16 || a.ld_q != a.d + 16 || !a.tstat || !a.qstat)
         return hipErrorInvalidValue;
+    if (f.kr > 0 && !(f.nw == 8 && f.rg == 2 && f.nbuf == 4)) return hipErrorInvalidValue;  // (fused_fn_k)
     void* args[] = {const_cast<GemmFilterArgs*>(&a)};
     const dim3 grid((unsigned)(a.g2 < 0 ? (int64_t)a.n_qtiles * a.nseg : (int64_t)a.p1_blocks + a.g2));
     hipError_t e = hipLaunchKernel(fused_ptr(a.d, f), grid, dim3(64 * f.nw), args, f.lds, st);

@@ -50,7 +50,6 @@ struct GemmFilterArgs {
     int k; int64_t seg_len; int nseg; int n_qtiles;
     float coef; float eta;
     uint32_t* gthr;
-    unsigned long long* timing;  // KNN_FILTER_TIMING builds: per-phase shader clocks (else NULL)
     int32_t* cnt;  // [nseg][nq] kept rows per (segment, query)
     CandRec* cand; int cap; int cap_seg;  // [nq][cap] candidate records
     const float4* tstat;  // fused filter, per 64-row tile: {max tn, max |t - rt|, max |rt|, 0}
@@ -137,18 +136,10 @@ bool knn_gemm_filter_supported(int elem, int row_bytes);
 // groups per wave, row groups per tile, min waves per SIMD (launch bounds), tile buffers,
 // queries per block, LDS bytes per block
 struct FilterPlan { int nw, qg, rg, minw, nbuf, bm; size_t lds; int kr = 0; /* fused: register-list length */ };
-// kernel-study overrides of the plan (KNN_FILTER_NBUF / KNN_FILTER_SHAPE, read once per
-// context by knn_create); NULL = the product plan
-struct FilterStudy {
-    int nbuf; char shape[8]; int pstep; /* -1 = plan default */
-    int kr = -1;      // fused filter: 0 = LDS heaps for every k, -1 = plan default
-};
-FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k, const FilterStudy* fs = nullptr);
-hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st,
-                                  const FilterStudy* fs = nullptr);
-size_t knn_gemm_filter_lds(int elem, int row_bytes, int k, const FilterStudy* fs = nullptr);
-hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks_per_cu,
-                                     const FilterStudy* fs = nullptr);
+FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k);
+hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st);
+size_t knn_gemm_filter_lds(int elem, int row_bytes, int k);
+hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks_per_cu);
 // fp32 rows [n][ld] (d % 4 == 0) -> bf16 rows [n][2d]: hi = rn(x), lo = rn(x - hi)
 hipError_t knn_launch_split_rows(const float* x, int64_t n, int ld, int d, uint16_t* out, hipStream_t st,
                                  const int32_t* gate = nullptr);
@@ -160,26 +151,17 @@ hipError_t knn_launch_rerun_decide(int32_t* ctrl, int64_t limit, hipStream_t st)
 hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st);
 // fused-norm filter (knn_fused.hip): rows augmented to d + 16 bf16 (k_aug_rows), d in {64, 128, 256}
 bool knn_fused_supported(int d);
-FilterPlan knn_fused_plan(int d, int k, const FilterStudy* fs = nullptr);  // nw == 0: k too large
-hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu, const FilterStudy* fs = nullptr);
+FilterPlan knn_fused_plan(int d, int k);  // nw == 0: k too large
+hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu);
 // fills a.p1_blocks / g2 / w2 / tiles64 for the balanced schedule over `slots` resident
 // blocks; returns the grid, *nseg = the most pieces one query tile gets.  (a.g2 = -1 and
 // a.seg_len / nseg instead: the segment schedule, n_qtiles * nseg blocks.)
 int knn_fused_schedule(GemmFilterArgs& a, int slots, int* nseg);
-hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st, const FilterStudy* fs = nullptr);
-// x [n][ld] (fp32 or bf16) -> bf16 [n][d + 16]: rn(scale * x) | split of norms[r] (or 1 1 1) | 0
-hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int ld, int d, const float* norms, float scale,
-                               uint16_t* out, hipStream_t st, const int32_t* gate = nullptr);
-// Starting thresholds of the GEMM filter (k_seed_threshold): gthr[q] = ordered k-th
-// smallest exact D from query q to ns <= KNN_SEED_MAX_ROWS rows spread over train.
-#define KNN_SEED_MAX_ROWS 2048
-struct SeedArgs {
-    const void* train; int64_t nt; int ld_t;
-    const void* test; int64_t nq; int ld_q; int d; int k;
-    int ns; int ld_lds;
-    uint32_t* gthr;
-};
-hipError_t knn_launch_seed_threshold(const SeedArgs& a, int elem, hipStream_t st);
+hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st);
+// x [n_valid][ld] (fp32 or bf16) -> bf16 [n][d + 16]: rn(scale * x) | split of norms[r] (or 1 1 1) | 0;
+// rows n_valid .. n-1 (train: padding to the 64-row tile grid) never pass the filter
+hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int64_t n_valid, int ld, int d, const float* norms,
+                               float scale, uint16_t* out, hipStream_t st, const int32_t* gate = nullptr);
 hipError_t knn_launch_merge(const MergeArgs& a, hipStream_t st);
 hipError_t knn_launch_generate(const GenerateArgs& a, hipStream_t st);
 // the bf16 filter's MFMA chain on [32][K] bf16 operands (certificate self-test)

@@ -605,13 +605,10 @@ __global__ __launch_bounds__(256) void k_round_rows(const float* __restrict__ x,
 // passes (slow path).  Kept rows go to this segment's slice of the query's candidate
 // list (LDS counter).
 // ---------------------------------------------------------------------------------
-#ifndef KNN_FILTER_DEFER
-#define KNN_FILTER_DEFER 1  // 8-wave shape: record passing values, flush them every KNN_FILTER_DEFER_EVERY tiles
-#endif
-#ifndef KNN_FILTER_PF
-#define KNN_FILTER_PF 6  // A-fragment prefetch depth in MFMAs (bf16)
-#endif
-
+// constants of the filter (measured against their alternatives in rounds 1-2)
+static constexpr int FILTER_PF = 6;            // A-fragment prefetch depth in MFMAs (bf16)
+static constexpr int FILTER_RQ = 4;            // deferred-queue depth per lane (8-wave shape)
+static constexpr int FILTER_DEFER_EVERY = 64;  // tiles between flushes of the deferred queues
 
 template <typename E, int RB, int MINW, int NBUF, int NW, int QG, int RG>
 __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a) {
@@ -628,7 +625,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
     constexpr int VPS = 16 / NS;                   // values per accumulator per k-step
     constexpr int NR = NBUF + 1;                   // norm ring slots: tiles it-1 .. it+NBUF-1
     static_assert(16 % NS == 0 && (NACC == 1 || NACC == 2) && (QG == 1 || RG == 1), "tile geometry");
-    static_assert(NBUF == 2 || NBUF == 3, "tile buffers");
+    static_assert(NBUF == 2, "tile buffers");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* tiles = smem;                                     // [NBUF][TILE]
     float* ring = reinterpret_cast<float*>(smem + NBUF * TILE);      // [NR][2][BN]: (1-c) tn, tn
@@ -691,8 +688,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 
     // LDS-DMA of one tile: slot P (16 B) of the padded image -> row P / SLOTS, slot P % SLOTS;
     // the pad slot (SLOTS-1) gets a duplicate of slot 0.  The last instruction may be
-    // partial (LAST_LANES active; each buffer has room for a whole one).  Rows past nt read
-    // row nt-1; their ring entries are +inf (tnorm/tnp are padded with +inf): never pass.
+    // partial (LAST_LANES active; each buffer has room for a whole one).  Rows past nt are
+    // the operand's pad rows; their ring entries are +inf (tnorm/tnp are padded with +inf):
+    // never pass.
     uint32_t doff[DMA_PER_WAVE];  // per-lane byte offsets of this wave's DMA slots in a tile
 #pragma unroll
     for (int i = 0; i < DMA_PER_WAVE; i++) {
@@ -700,10 +698,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
         const int row = min(P / SLOTS, BN - 1), sl = P % SLOTS;
         doff[i] = (uint32_t)(row * ldb + 16 * (sl == SLOTS - 1 ? 0 : sl));
     }
-    // vector-memory ops this wave issues per tile (its DMA instructions + one norm load)
-    int n_dma_wave = (wave >= NW - 2) ? 1 : 0;
-#pragma unroll
-    for (int i = 0; i < DMA_PER_WAVE; i++) n_dma_wave += (wave + NW * i < DMA_INS) ? 1 : 0;
     // DMA piece i < DMA_PER_WAVE: this wave's i-th 1 KiB instruction of the tile; piece
     // DMA_PER_WAVE: the tile's norm terms (two waves).  The step issues the pieces spread
     // between its MFMAs: issued as one burst after the barrier, every wave queued behind
@@ -712,26 +706,20 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
     // LDS byte offsets as plain 32-bit SGPR values (one generic -> LDS conversion, here)
     const uint32_t lds_tiles = __builtin_amdgcn_readfirstlane(lds_addr(tiles));
     const uint32_t lds_ring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
-    // one tile's DMA: uniform source row pointer, LDS buffer / ring offsets, full-tile flag
-    struct DmaTile { const unsigned char* src; uint32_t lds, lring; int64_t r0; bool full; };
+    // one tile's DMA: uniform source row pointer, LDS buffer / ring offsets.  Every tile is
+    // whole: the operand rows cover the 64-row tile grid (run_gemm pads them), so a piece is
+    // always the scalar tile base + this lane's fixed offset
+    struct DmaTile { const unsigned char* src; uint32_t lds, lring; int64_t r0; };
     auto dma_desc = [&](int buf, int slot, int64_t r0) -> DmaTile {
         return DmaTile{trainb + r0 * ldb, lds_tiles + (uint32_t)(buf * TILE),
-                       lds_ring + (uint32_t)(slot * 2 * BN * 4), r0, r0 + BN <= a.nt};
+                       lds_ring + (uint32_t)(slot * 2 * BN * 4), r0};
     };
     auto dma_piece = [&](int i, const DmaTile& d) __attribute__((always_inline)) {
         if (i < DMA_PER_WAVE) {
             const int ins = wave + NW * i;
             if (ins < DMA_INS) {
                 if (i == DMA_PER_WAVE - 1 && ins == DMA_INS - 1 && lane >= FT::LAST_LANES) return;
-                const uint32_t dst = d.lds + (uint32_t)ins * 1024u;
-                if (d.full) {
-                    dma16s(doff[i], d.src, dst);
-                } else {
-                    const int P = ins * 64 + lane;
-                    const int row = P / SLOTS, sl = P % SLOTS;
-                    const int64_t t = min(d.r0 + row, a.nt - 1);
-                    dma16(trainb + t * ldb + 16 * (sl == SLOTS - 1 ? 0 : sl), dst);
-                }
+                dma16s(doff[i], d.src, d.lds + (uint32_t)ins * 1024u);
             }
         } else if (lane < BN) {
             if (wave == NW - 2)
@@ -778,24 +766,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
                 t4[ta] = *reinterpret_cast<const float4*>(tnpY + 32 * ta + 8 * (reg >> 2) + 4 * h);
             return fmaf(-2.0f, Y[acc][reg], f4get(t4[ta], reg & 3));
         };
-#if KNN_FILTER_PK
-        // study variant: two adjacent fast-test values (v even) in one v_pk_fma_f32 (the same
-        // correctly rounded fma per element), folded into the running minimum by v_min3_f32
-        auto epi_y2 = [&](int v, float& m) __attribute__((always_inline)) {
-            const int acc = v >> 4, reg = v & 15, ta = rg_of(acc);
-            if ((reg & 3) == 0 && (RG == 2 || acc == 0))
-                t4[ta] = *reinterpret_cast<const float4*>(tnpY + 32 * ta + 8 * (reg >> 2) + 4 * h);
-            const floatx2 tt = (reg & 2) ? floatx2{t4[ta].z, t4[ta].w} : floatx2{t4[ta].x, t4[ta].y};
-            const floatx2 yy = floatx2{Y[acc][reg], Y[acc][reg + 1]};
-            floatx2 y;
-            asm volatile("v_pk_fma_f32 %0, %1, -2.0, %2 op_sel_hi:[1,0,1]" : "=v"(y) : "v"(yy), "v"(tt));
-            asm volatile("v_min3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(m), "v"(y.x), "v"(y.y));
-        };
-#endif
         if constexpr (BF) {
             // one 32x32x16 MFMA per 16-B fragment: prefetch the A fragments PF k-steps ahead
             // and interleave the previous tile's fast test between the MFMAs
-            constexpr int PF = KNN_FILTER_PF / NACC;  // covers ~KNN_FILTER_PF x 32 MFMA cycles of LDS latency
+            constexpr int PF = FILTER_PF / NACC;  // covers ~FILTER_PF x 32 MFMA cycles of LDS latency
             uint4 xa[NS], xb[NS];
 #pragma unroll
             for (int s = 0; s < PF && s < NS; s++) {
@@ -828,19 +802,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
                     }
 #pragma unroll
                     for (int vv = 0; vv < VPS; vv++) {
-#ifndef KNN_ABLATE_NO_EPI
-#if KNN_FILTER_PK
-                        if constexpr (VPS % 2 == 0) {
-                            if (vv % 2 == 0) epi_y2(16 * c + s * VPS + vv, mn[c]);
-                            continue;
+                        if (!KNN_STUDY_NO_EPI) {
+                            const float y = epi_y(16 * c + s * VPS + vv);
+                            asm volatile("" ::"v"(y));  // computed here, beside this MFMA
+                            mn[c] = fminf(mn[c], y);
+                        } else {
+                            asm volatile("" ::"v"(Y[c][(s * VPS + vv) & 15]));
                         }
-#endif
-                        const float y = epi_y(16 * c + s * VPS + vv);
-                        asm volatile("" ::"v"(y));  // computed here, beside this MFMA
-                        mn[c] = fminf(mn[c], y);
-#else
-                        asm volatile("" ::"v"(Y[c][(s * VPS + vv) & 15]));
-#endif
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);  // keep this k-step's order (prefetch, MFMA, VALU)
@@ -862,11 +830,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
                 for (int c = 0; c < NACC; c++)
 #pragma unroll
                     for (int vv = 0; vv < VPS; vv++) {
-#ifndef KNN_ABLATE_NO_EPI
-                        mn[c] = fminf(mn[c], epi_y(16 * c + s * VPS + vv));
-#else
-                        asm volatile("" ::"v"(Y[c][(s * VPS + vv) & 15]));
-#endif
+                        if (!KNN_STUDY_NO_EPI) mn[c] = fminf(mn[c], epi_y(16 * c + s * VPS + vv));
+                        else asm volatile("" ::"v"(Y[c][(s * VPS + vv) & 15]));
                     }
             }
         }
@@ -879,14 +844,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
     // exact re-check of tile tp (accumulators Y) for the values whose fast test passed:
     // a bit-mask pass, then a wave-uniform loop over the set bits (the value is picked by
     // a select chain, so the accumulators are never indexed dynamically)
-#ifdef KNN_FILTER_TIMING
-    // per-phase shader clocks of this wave: [0] wait+barrier, [1] DMA issue, [2] step,
-    // [3] slow, [4] slow after tile 4096, [5] slow invocations, [6] mask, [7] turn loops
-    unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define KNN_TSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#else
-#define KNN_TSTAMP(v)
-#endif
     // keep candidate (L, U) of global row t for query group g of this lane: the exact test
     // against the current threshold, the candidate store into this lane half's sub-slice,
     // and, if U beats the heap root, a sift-down of the 4-ary max-heap (node n >= 1 in
@@ -988,9 +945,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 
     // immediate slow path: every passing value of tile tp is accepted now
     auto slow = [&](floatx16 (&Y)[NACC], int tp) {
-        KNN_TSTAMP(ts0);
         const uint32_t m = pass_mask(Y, tp);
-        KNN_TSTAMP(ts1);
         // the two lanes of a query take turns, so each heap has one writer at a time; the
         // candidate slot counters are per lane (each lane half owns a sub-slice)
         for (int hh = 0; hh < 2; hh++) {
@@ -1008,10 +963,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
             }
             sync_roots(hh);
         }
-#ifdef KNN_FILTER_TIMING
-        KNN_TSTAMP(ts2);
-        tph[5] += 1; tph[6] += ts1 - ts0; tph[7] += ts2 - ts1;
-#endif
         publish();
     };
 
@@ -1021,10 +972,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
     // tile (one wave's heap work then no longer holds the other seven at each barrier),
     // or at once when some lane's queue is full.  A threshold that waits for the flush is
     // stale but still valid (it only ever tightens).
-#ifndef KNN_FILTER_RQ
-#define KNN_FILTER_RQ 4  // deferred-queue depth per lane
-#endif
-    constexpr int RQ = KNN_FILTER_RQ;
+    constexpr int RQ = FILTER_RQ;
     float qL[RQ], qU[RQ];
     int qT[RQ];
     bool qG[RQ];
@@ -1044,9 +992,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
         publish();
     };
     auto record = [&](floatx16 (&Y)[NACC], int tp) {
-        KNN_TSTAMP(ts0);
         uint32_t mm = pass_mask(Y, tp);
-        KNN_TSTAMP(ts1);
         while (__ballot(mm != 0u)) {
             if (__ballot(qcnt >= RQ && mm != 0u)) flush();
             if (mm != 0u) {
@@ -1064,10 +1010,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
                 }
             }
         }
-#ifdef KNN_FILTER_TIMING
-        KNN_TSTAMP(ts2);
-        tph[5] += 1; tph[6] += ts1 - ts0; tph[7] += ts2 - ts1;
-#endif
     };
 
     const int ntiles = (row_end > row_begin) ? (int)((row_end - row_begin + BN - 1) / BN) : 0;
@@ -1078,23 +1020,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 #pragma unroll
     for (int p = 0; p < NBUF - 1; p++)
         if (p < ntiles) dma_tile(p, p, row_begin + (int64_t)p * BN);
-    // NBUF = 3 issues the next DMA after the slow path, so the slow path's stores are older
-    // than it and the barrier's counted wait still leaves that DMA in flight (vmcnt retires in
-    // issue order).  NBUF = 2 issues it inside the step: it must land by the next barrier.
-#ifndef KNN_FILTER_EARLY_DMA
-#define KNN_FILTER_EARLY_DMA 0  // NBUF = 3: issue the DMA inside the step as NBUF = 2 does
-#endif
-    // (early: a wave that stored after the DMA waits for everything at the next barrier)
-    constexpr bool LATE_DMA = NBUF == 3 && !KNN_FILTER_EARLY_DMA;
-#ifndef KNN_FILTER_DEFER_W4
-#define KNN_FILTER_DEFER_W4 0  // kernel studies: the deferred slow path in 4-wave blocks too
-#endif
-    constexpr bool DEFER = (NW == 8 || KNN_FILTER_DEFER_W4) && KNN_FILTER_DEFER;  // deferred slow path (see record())
-#ifndef KNN_FILTER_DEFER_EVERY
-#define KNN_FILTER_DEFER_EVERY 64  // tiles between flushes of the deferred queues (16: A 37.1 ms, 32: 36.4, 64: 35.8)
-#endif
-    constexpr int DEFER_EVERY = KNN_FILTER_DEFER_EVERY;
-    bool dirty = false;  // NBUF = 2: this wave issued vector-memory ops after the newest DMA
+    // the step issues the next tile's DMA between its MFMAs: it must land by the next barrier
+    constexpr bool DEFER = NW == 8;  // deferred slow path (see record())
+    constexpr int DEFER_EVERY = FILTER_DEFER_EVERY;
     auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
         const int64_t r0 = row_begin + (int64_t)it * BN;
         if ((it & 63) == 63 && a.nseg > 1) {
@@ -1107,45 +1035,22 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
                 }
             }
         }
-        // tile it landed (NBUF = 3: tile it+1's DMA may stay in flight); every wave is done
-        // with the buffer / ring slot the next DMA overwrites (tile it-1's, read last iteration)
-        const bool keep_next = NBUF == 3 && it + 1 < ntiles && (LATE_DMA || !dirty);
-        KNN_TSTAMP(t0);
-        wait_dma_barrier(keep_next ? n_dma_wave : 0);
-        dirty = false;
-        KNN_TSTAMP(t1);
-#ifndef KNN_ABLATE_NO_DMA
-        const bool dma_on = it + NBUF - 1 < ntiles;
-#else
-        const bool dma_on = false;
-#endif
-        KNN_TSTAMP(t2);
+        // tile it landed; every wave is done with the buffer / ring slot the next DMA
+        // overwrites (tile it-1's, read last iteration)
+        wait_dma_barrier(0);
+        const bool dma_on = !KNN_STUDY_NO_DMA && it + NBUF - 1 < ntiles;
         const DmaTile dd = dma_desc((it + NBUF - 1) % NBUF, (it + NBUF - 1) % NR, r0 + (int64_t)(NBUF - 1) * BN);
-        const bool any = step(X, Y, it % NBUF, (it + NR - 1) % NR, dma_on && !LATE_DMA, dd);
-        KNN_TSTAMP(t3);
-#ifndef KNN_ABLATE_NO_SLOW
-        if constexpr (DEFER) {
-            if (any && it > 0) record(Y, it - 1);
-            if ((it & (DEFER_EVERY - 1)) == DEFER_EVERY - 1 && __ballot(qcnt > 0)) {
-                flush();
-                dirty = true;
+        const bool any = step(X, Y, it % NBUF, (it + NR - 1) % NR, dma_on, dd);
+        if (!KNN_STUDY_NO_SLOW) {
+            if constexpr (DEFER) {
+                if (any && it > 0) record(Y, it - 1);
+                if ((it & (DEFER_EVERY - 1)) == DEFER_EVERY - 1 && __ballot(qcnt > 0)) flush();
+            } else if (any && it > 0) {
+                slow(Y, it - 1);
             }
-        } else if (any && it > 0) {
-            slow(Y, it - 1);
-            dirty = true;
+        } else if (any) {
+            asm volatile("" ::"v"(Y[0][0]), "v"(Y[NACC - 1][3]));
         }
-#else
-        if (any) asm volatile("" ::"v"(Y[0][0]), "v"(Y[NACC - 1][3]));
-#endif
-        if (LATE_DMA && dma_on) {
-#pragma unroll
-            for (int i = 0; i < NPIECE; i++) dma_piece(i, dd);
-        }
-#ifdef KNN_FILTER_TIMING
-        KNN_TSTAMP(t4);
-        tph[0] += t1 - t0; tph[1] += t2 - t1; tph[2] += t3 - t2; tph[3] += t4 - t3;
-        if (it >= 4096) tph[4] += t4 - t3;  // slow path after the first 4096 tiles
-#endif
     };
     for (int it = 0; it < ntiles; it += 2) {
         iter(accA, accB, it);
@@ -1181,18 +1086,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 #pragma unroll
     for (int g = 0; g < QG; g++)
         if (qvalid[g]) a.cnt[(int64_t)(2 * seg + h) * a.nq + q[g]] = ccnt[g];
-#ifdef KNN_FILTER_TIMING
-    if (a.timing && lane == 0) {
-#pragma unroll
-        for (int i = 0; i < 4; i++) atomicAdd(&a.timing[i], tph[i]);
-        atomicAdd(&a.timing[4], 1ull);
-        atomicAdd(&a.timing[5], tph[4]);
-        atomicAdd(&a.timing[6], tph[5]);
-        atomicAdd(&a.timing[7], tph[6]);
-        atomicAdd(&a.timing[8], tph[7]);
-    }
-#endif
-#undef KNN_TSTAMP
 }
 
 // ---------------------------------------------------------------------------------
@@ -1426,11 +1319,12 @@ __global__ __launch_bounds__(256) void k_merge_vote(MergeArgs a) {
                 const int32_t ix = rec[k + e];
                 if (ix >= 0) key = make_key(__int_as_float(rec[e]), (uint32_t)ix);
             }
+            // a source list ascends by key (a shard's exact top-k, or a segment's), so a batch
+            // is a sorted run: passing keys are its prefix, none past the first that fails
             const bool pass = key < kth;
-            if (__ballot(pass)) {
-                topk_merge<R>(T, pass ? key : KEY_NONE);
-                kth = list_at(T, k - 1);
-            }
+            if (!__ballot(pass)) break;
+            topk_merge_sorted<R>(T, pass ? key : KEY_NONE);
+            kth = list_at(T, k - 1);
         }
     }
     if (a.labels) {
@@ -1765,11 +1659,8 @@ static size_t gemm_filter_lds_of(int row_bytes, int k, int nw, int qg, int rg, i
 //    allows, else 32-row tiles, triple-buffered when the LDS allows (large k: big heaps).
 //    Larger k that does not fit falls back to the fp32 shape.
 //  bf16 rows of 128 bytes (64 features): 4 waves x 32 queries, 64-row tiles, two blocks per CU.
-// KNN_FILTER_NBUF=2|3 and KNN_FILTER_SHAPE=w8r2|w8|w4r1|w4q2|w4 (bf16/split) force a shape (kernel studies).
-FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k, const FilterStudy* fs) {
+FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k) {
     const size_t cap = 160 * 1024;
-    const int force_nb = fs ? fs->nbuf : 0;
-    const std::string shape = fs ? fs->shape : "";
     auto fits = [&](int nw, int qg, int rg, int nbuf, size_t limit) {
         return gemm_filter_lds_of(row_bytes, k, nw, qg, rg, nbuf) <= limit;
     };
@@ -1777,42 +1668,23 @@ FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k, const FilterStud
         FilterPlan f{nw, qg, rg, minw, nbuf, 32 * qg * nw, gemm_filter_lds_of(row_bytes, k, nw, qg, rg, nbuf)};
         return f;
     };
-    if (elem != ELEM_F32 && shape.empty() && row_bytes == 128 && fits(4, 1, 2, 2, cap / 2)) {
+    if (elem != ELEM_F32) {
         // short rows (64 bf16 features: 4 MFMAs per 32x32 block and tile): the per-tile
         // barrier and fast test outweigh the MFMAs, so two 4-wave blocks per CU hide each
-        // other's synchronisation.  Measured on B (rounded bf16, k=32): 880 ms vs 1062 ms
-        // for w8r2 on the same box; on A (128 features) w8r2 stays ahead (37.0 vs 40.7 ms)
-        return make(4, 1, 2, 2, 2);
-    }
-    if (elem != ELEM_F32 && (shape.empty() || shape == "w8r2")) {
+        // other's synchronisation (B, rounded bf16, k=32: 880 ms vs 1062 ms for 8 waves)
+        if (row_bytes == 128 && fits(4, 1, 2, 2, cap / 2)) return make(4, 1, 2, 2, 2);
         // 8 waves x 32 queries over 64-row tiles (two accumulators per wave): half the
-        // barriers, waits and DMA-issue rounds per MFMA of the 32-row shape.  Double
-        // buffered: measured faster than triple on A and B (63 vs 69 ms, 1.42 vs 1.53 s)
-        if (force_nb != 3 && fits(8, 1, 2, 2, cap)) return make(8, 1, 2, 2, 2);
-        if (force_nb == 3 && fits(8, 1, 2, 3, cap)) return make(8, 1, 2, 2, 3);
+        // barriers, waits and DMA-issue rounds per MFMA of the 32-row shape; 32-row tiles
+        // when the heaps of a large k leave no room
+        if (fits(8, 1, 2, 2, cap)) return make(8, 1, 2, 2, 2);
+        if (fits(8, 1, 1, 2, cap)) return make(8, 1, 1, 2, 2);
     }
-    if (elem != ELEM_F32 && (shape.empty() || shape == "w8")) {
-        if (force_nb != 2 && fits(8, 1, 1, 3, cap)) return make(8, 1, 1, 2, 3);
-        if (force_nb != 3 && fits(8, 1, 1, 2, cap)) return make(8, 1, 1, 2, 2);
-    }
-    if (elem != ELEM_F32 && shape == "w4r1") {
-        // 4 waves x 32 queries over 32-row tiles, two blocks per CU: the two waves of a
-        // SIMD belong to different blocks, so one block's barrier / slow path runs under
-        // the other's MFMAs (at twice the L2 -> LDS bytes per FLOP of the 8-wave block)
-        if (force_nb != 2 && fits(4, 1, 1, 3, cap / 2)) return make(4, 1, 1, 2, 3);
-        if (fits(4, 1, 1, 2, cap / 2)) return make(4, 1, 1, 2, 2);
-    }
-    if (elem != ELEM_F32 && shape == "w4q2") {
-        if (force_nb != 2 && fits(4, 2, 1, 3, cap)) return make(4, 2, 1, 1, 3);
-        if (fits(4, 2, 1, 2, cap)) return make(4, 2, 1, 1, 2);
-    }
-    if (force_nb != 3 && fits(4, 1, 2, 2, cap / 2)) return make(4, 1, 2, 2, 2);
-    if (force_nb != 2 && fits(4, 1, 2, 3, cap)) return make(4, 1, 2, 1, 3);
+    if (fits(4, 1, 2, 2, cap / 2)) return make(4, 1, 2, 2, 2);
     return make(4, 1, 2, 1, 2);
 }
 
-size_t knn_gemm_filter_lds(int elem, int row_bytes, int k, const FilterStudy* fs) {
-    return knn_gemm_filter_plan(elem, row_bytes, k, fs).lds;
+size_t knn_gemm_filter_lds(int elem, int row_bytes, int k) {
+    return knn_gemm_filter_plan(elem, row_bytes, k).lds;
 }
 
 bool knn_gemm_filter_supported(int elem, int row_bytes) {
@@ -1822,15 +1694,11 @@ bool knn_gemm_filter_supported(int elem, int row_bytes) {
 
 template <typename E, int RB>
 static const void* gemm_filter_fn(const FilterPlan& f) {
-#define KNN_FILTER_FN(MINW, NBUF, NW, QG, RG) reinterpret_cast<const void*>(&k_gemm_filter<E, RB, MINW, NBUF, NW, QG, RG>)
+#define KNN_FILTER_FN(MINW, NW, RG) reinterpret_cast<const void*>(&k_gemm_filter<E, RB, MINW, 2, NW, 1, RG>)
     if constexpr (sizeof(E) == 2) {
-        if (f.nw == 8 && f.rg == 2) return f.nbuf == 3 ? KNN_FILTER_FN(2, 3, 8, 1, 2) : KNN_FILTER_FN(2, 2, 8, 1, 2);
-        if (f.nw == 8) return f.nbuf == 3 ? KNN_FILTER_FN(2, 3, 8, 1, 1) : KNN_FILTER_FN(2, 2, 8, 1, 1);
-        if (f.rg == 1 && f.qg == 1) return f.nbuf == 3 ? KNN_FILTER_FN(2, 3, 4, 1, 1) : KNN_FILTER_FN(2, 2, 4, 1, 1);
-        if (f.qg == 2) return f.nbuf == 3 ? KNN_FILTER_FN(1, 3, 4, 2, 1) : KNN_FILTER_FN(1, 2, 4, 2, 1);
+        if (f.nw == 8) return f.rg == 2 ? KNN_FILTER_FN(2, 8, 2) : KNN_FILTER_FN(2, 8, 1);
     }
-    if (f.minw == 2) return KNN_FILTER_FN(2, 2, 4, 1, 2);
-    return f.nbuf == 3 ? KNN_FILTER_FN(1, 3, 4, 1, 2) : KNN_FILTER_FN(1, 2, 4, 1, 2);
+    return f.minw == 2 ? KNN_FILTER_FN(2, 4, 2) : KNN_FILTER_FN(1, 4, 2);
 #undef KNN_FILTER_FN
 }
 
@@ -1845,17 +1713,16 @@ static const void* gemm_filter_ptr(int elem, int row_bytes, const FilterPlan& f)
          : row_bytes == 256 ? gemm_filter_fn<float, 256>(f) : gemm_filter_fn<float, 512>(f);
 }
 
-hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks_per_cu, const FilterStudy* fs) {
+hipError_t knn_gemm_filter_occupancy(int elem, int row_bytes, int k, int* blocks_per_cu) {
     if (!knn_gemm_filter_supported(elem, row_bytes)) return hipErrorInvalidValue;
-    const FilterPlan f = knn_gemm_filter_plan(elem, row_bytes, k, fs);
+    const FilterPlan f = knn_gemm_filter_plan(elem, row_bytes, k);
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, gemm_filter_ptr(elem, row_bytes, f),
                                                         64 * f.nw, f.lds);
 }
 
-hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st,
-                                  const FilterStudy* fs) {
+hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st) {
     if (!knn_gemm_filter_supported(elem, row_bytes)) return hipErrorInvalidValue;
-    const FilterPlan f = knn_gemm_filter_plan(elem, row_bytes, a.k, fs);
+    const FilterPlan f = knn_gemm_filter_plan(elem, row_bytes, a.k);
     const void* fn = gemm_filter_ptr(elem, row_bytes, f);
     void* args[] = {const_cast<GemmFilterArgs*>(&a)};
     const dim3 grid((unsigned)(a.n_qtiles * a.nseg));
@@ -1895,68 +1762,6 @@ hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st) {
     return a.elem == ELEM_BF16 ? launch_rescore_e<bf16_t>(a, st) : launch_rescore_e<float>(a, st);
 }
 
-// ---------------------------------------------------------------------------------
-// k_seed_threshold<E>: a valid starting threshold for the GEMM filter.  One wave per
-// query computes the exact direct-form D (direct_dist, as the rescore does) to ns rows
-// spread evenly over the train set and stores the k-th smallest as ordered bits in gthr.
-// Any k real rows have a k-th distance >= D_(k), the true k-th distance, so every row of
-// the exact top-k still has L <= D <= D_(k) <= thr and is kept: the filter only starts
-// its scan from this bound instead of +inf (no heap-filling phase of all-passing tiles).
-// A D that is not < FLT_MAX never counts; with fewer than k finite D, gthr stays +inf.
-// LDS per wave: the query row widened to fp32 [ld_lds].
-// ---------------------------------------------------------------------------------
-constexpr int SEED_PER_LANE = KNN_SEED_MAX_ROWS / 64;
-template <typename E>
-__global__ __launch_bounds__(256) void k_seed_threshold(SeedArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int lane = lane_id();
-    const int wave = threadIdx.x >> 6;
-    float* qs = reinterpret_cast<float*>(smem) + (size_t)wave * a.ld_lds;
-    const int64_t q = (int64_t)blockIdx.x * 4 + wave;
-    if (q >= a.nq) return;
-    const E* train = reinterpret_cast<const E*>(a.train);
-    const E* test = reinterpret_cast<const E*>(a.test);
-    for (int i = lane; i < a.d; i += 64) qs[i] = widen(test[q * a.ld_q + i]);
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    uint32_t o[SEED_PER_LANE];
-    int valid = 0;
-#pragma unroll
-    for (int i = 0; i < SEED_PER_LANE; i++) {
-        const int sidx = lane + 64 * i;
-        uint32_t v = 0xffffffffu;
-        if (sidx < a.ns) {
-            const int64_t t = (int64_t)sidx * a.nt / a.ns;  // distinct rows: ns <= nt
-            const float D = direct_dist(qs, train + t * a.ld_t, a.d);
-            if (D < FLT_MAX) v = f2o(D);
-        }
-        o[i] = v;
-        valid += __popcll(__ballot(v != 0xffffffffu));
-    }
-    if (valid < a.k) return;
-    // smallest x with #{o <= x} >= k
-    uint32_t lo = 0u, hi = 0xfffffffeu;
-    while (lo < hi) {
-        const uint32_t mid = lo + ((hi - lo) >> 1);
-        int c = 0;
-#pragma unroll
-        for (int i = 0; i < SEED_PER_LANE; i++) c += __popcll(__ballot(o[i] <= mid));
-        if (c >= a.k) hi = mid; else lo = mid + 1;
-    }
-    if (lane == 0) a.gthr[q] = lo;
-}
-
-hipError_t knn_launch_seed_threshold(const SeedArgs& a, int elem, hipStream_t st) {
-    if (a.nq <= 0 || a.ns < a.k || a.ns > a.nt || a.ns > KNN_SEED_MAX_ROWS || a.ld_lds < a.d) return hipErrorInvalidValue;
-    const unsigned grid = (unsigned)((a.nq + 3) / 4);
-    const size_t lds = 4 * (size_t)a.ld_lds * sizeof(float);
-    if (elem == ELEM_BF16)
-        hipLaunchKernelGGL(k_seed_threshold<bf16_t>, dim3(grid), dim3(256), lds, st, a);
-    else
-        hipLaunchKernelGGL(k_seed_threshold<float>, dim3(grid), dim3(256), lds, st, a);
-    KNN_LAUNCH_CHECK();
-    return hipSuccess;
-}
 
 template <int R>
 static hipError_t launch_merge_r(const MergeArgs& a, hipStream_t st) {

@@ -126,3 +126,50 @@ def test_loaded_library_is_this_trees(knn):
     (knn_build_id() == build_id.py's hash of the tree)."""
     built, tree = knn.build_id()
     assert built == tree
+
+
+def test_cache_survives_reused_temporaries(knn, oracle):
+    """cache_train with inputs _dataset must convert (float64 features, int64 labels): each
+    call's temporaries are new arrays that the allocator may place at a freed temporary's
+    address; the results must still be each call's own (the Context holds the keyed arrays)."""
+    ctx = knn.Context(0, cache_train=True)
+    try:
+        for seed in (71, 72, 73):
+            tr, tl, te = _data(oracle, nt=6000, nq=300, d=64, seed=seed)
+            bad, opred, odist, oidx = oracle.knn(tr, tl, te, 5, 10)
+            got = ctx.predict(tr.astype(np.float64), tl.astype(np.int64), te.astype(np.float64), 5, 10, topk=True)
+            assert _same(got, (opred, odist, oidx)), seed
+    finally:
+        ctx.close()
+
+
+def test_cpp_cache_keyed_by_flat_view(knn, oracle, tmp_path):
+    """The C++ KNN() contexts cache train uploads: datasets of one shape parsed, classified
+    and freed in turn (their pinned buffers reused at the same address) must each give their
+    own predictions (tests/cpp/flat_cache_check.cpp)."""
+    import os
+    import subprocess
+    from conftest import PKG_DIR
+    exe = os.path.join(PKG_DIR, "build", "flat_cache_check")
+    if not os.path.exists(exe):
+        pytest.skip("build/flat_cache_check not built (make -C knn-using-p_threads-and-mpi_amd)")
+    args, want = [], []
+    for seed in (81, 82, 83):
+        tr, tl, te = _data(oracle, nt=3000, nq=200, d=16, seed=seed)
+        paths = []
+        for name, f, lab in (("train", tr, tl), ("test", te, np.zeros(len(te), np.int32))):
+            p = tmp_path / f"{name}{seed}.arff"
+            with open(p, "w") as fh:
+                fh.write("@relation r\n" + "".join(f"@attribute a{i} numeric\n" for i in range(16)))
+                fh.write("@attribute class numeric\n@data\n")
+                for r in range(len(f)):
+                    fh.write(",".join(f"{v:.9g}" for v in f[r]) + f",{lab[r]}\n")
+            paths.append(str(p))
+        args += paths
+        want.append(oracle.knn(tr, tl, te, 5, 10)[1])
+    r = subprocess.run([exe, "5"] + args, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 3
+    for line, w in zip(lines, want):
+        assert np.array_equal(np.array(line.split(), np.int32), w)

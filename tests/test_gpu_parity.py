@@ -107,29 +107,6 @@ def test_gemm_duplicates_and_ties(knn, oracle, ctxs):
             assert np.array_equal(idx, oidx) and np.array_equal(pred, opred)
 
 
-@pytest.mark.parametrize("d,k,nt,nq", [(128, 10, 20000, 300), (64, 32, 30000, 200), (256, 100, 9000, 70)])
-def test_seeded_thresholds(knn, oracle, ctxs, monkeypatch, d, k, nt, nq):
-    """Study option KNN_FILTER_SEED=1 (k_seed_threshold): the filter starts from the exact
-    k-th distance to a spread train sample; results stay bit-identical, duplicates included."""
-    monkeypatch.setenv("KNN_FILTER_SEED", "1")
-    tr, tl = oracle.gen(11, 0, 0, nt, d)
-    te, _ = oracle.gen(11, 1, 0, nq, d)
-    tr[1::7] = tr[0]  # many exact ties among the sampled rows
-    bad, opred, odist, oidx = oracle.knn(tr, tl, te, k, 10)
-    assert bad == 0
-    for algo in ("gemm", "gemm_split", "gemm_bf16", "auto"):
-        ctx = knn.Context(0, algo=algo, profile=True)  # profiled: the stage list names "seed"
-        try:
-            pred, dist, idx = ctx.predict(tr, tl, te, k, 10, topk=True)
-            if algo != "auto" and d in GEMM_DIMS[algo]:
-                assert "seed" in ctx.stage_times(), algo
-        finally:
-            ctx.close()
-        assert np.array_equal(idx, oidx), algo
-        assert np.array_equal(dist.view(np.uint32), odist.view(np.uint32)), algo
-        assert np.array_equal(pred, opred), algo
-
-
 @pytest.mark.parametrize("su", [64, 128])
 def test_rescore_small_staging(knn, oracle, monkeypatch, su):
     """k_rescore stages about twice the expected candidates per query in LDS; longer lists
