@@ -188,6 +188,17 @@ def _device_dataset(feat, labels=None, d=None):
                        ld, _tensor_dtype(feat))
 
 
+def _stream_arg(stream, tensor):
+    """The HIP stream a device call is enqueued on: the caller's, else torch's current stream
+    of the tensor's device -- so the call is ordered after the torch work that produced its
+    inputs (a copy, a dtype conversion, a clone) and before the torch work that reads its
+    outputs, with no extra synchronisation."""
+    if stream is None and tensor is not None and getattr(tensor, "is_cuda", False):
+        import torch
+        stream = torch.cuda.current_stream(tensor.device).cuda_stream
+    return None if stream is None else ctypes.c_void_p(stream)
+
+
 def _outputs(nq, k, pred=None, dist=None, idx=None):
     """Type/shape checks of device outputs (pred int32 [nq], dist float32 / idx int32 [nq][k])."""
     import torch
@@ -340,7 +351,7 @@ class Context:
         self._check(self.lib.knn_predict_device(
             self.h, ctypes.byref(tr), ctypes.byref(te), k, num_classes, pred.data_ptr(),
             None if dist is None else dist.data_ptr(), None if idx is None else idx.data_ptr(),
-            None if stream is None else ctypes.c_void_p(stream)))
+            _stream_arg(stream, test)))
 
     def shard_topk_device(self, train, labels, test, k, num_classes, idx_base, rec, stream=None, d=None):
         """Exact k nearest rows of one train shard for every query (knn_shard_topk_device).
@@ -353,7 +364,7 @@ class Context:
         _check_tensor(rec, "rec", torch.int32)
         self._check(self.lib.knn_shard_topk_device(
             self.h, ctypes.byref(tr), ctypes.byref(te), k, num_classes, idx_base, rec.data_ptr(),
-            None if stream is None else ctypes.c_void_p(stream)))
+            _stream_arg(stream, test)))
 
     def merge_vote_device(self, rec, k, num_classes, pred, dist=None, idx=None, stream=None):
         """Merge nsrc per-shard neighbour lists rec [nsrc][nq][3][k] and vote (knn_merge_vote_device)."""
@@ -366,7 +377,7 @@ class Context:
         self._check(self.lib.knn_merge_vote_device(
             self.h, nsrc, nq, k, num_classes, rec.data_ptr(), pred.data_ptr(),
             None if dist is None else dist.data_ptr(), None if idx is None else idx.data_ptr(),
-            None if stream is None else ctypes.c_void_p(stream)))
+            _stream_arg(stream, rec)))
 
     def generate(self, feat, labels, row0, d, kind, seed, stream_id, num_classes, dtype=None,
                  stream=None):
@@ -376,7 +387,7 @@ class Context:
         self._check(self.lib.knn_generate(
             self.h, feat.data_ptr(), None if labels is None else labels.data_ptr(), row0,
             feat.shape[0], d, feat.shape[1], dtype, kind, seed, stream_id, num_classes,
-            None if stream is None else ctypes.c_void_p(stream)))
+            _stream_arg(stream, feat)))
 
     def confusion_matrix_device(self, pred, labels, num_classes, cm=None, stream=None):
         """computeConfusionMatrix / computeAccuracy (main.cpp:87-112) on device tensors:
@@ -389,7 +400,7 @@ class Context:
         corr = torch.zeros(1, dtype=torch.int64, device=pred.device)
         self._check(self.lib.knn_confusion_matrix_device(
             self.h, pred.data_ptr(), labels.data_ptr(), pred.shape[0], num_classes, cm.data_ptr(),
-            corr.data_ptr(), None if stream is None else ctypes.c_void_p(stream)))
+            corr.data_ptr(), _stream_arg(stream, pred)))
         n = pred.shape[0]
         return cm, float(np.float32(int(corr.item())) / np.float32(n)) if n else float("nan")
 
@@ -402,7 +413,7 @@ class Context:
         a, b = a.contiguous(), b.contiguous()
         out = torch.empty((32, 32), dtype=torch.float32, device=a.device)
         self._check(self.lib.knn_mfma_probe_bf16(self.h, a.data_ptr(), b.data_ptr(), a.shape[1], out.data_ptr(),
-                                                 None if stream is None else ctypes.c_void_p(stream)))
+                                                 _stream_arg(stream, a)))
         return out
 
     def set_generation(self, generation):
@@ -493,7 +504,7 @@ class Comm:
         st = self.lib.knn_predict_train_sharded(
             self.ctx.h, self.h, ctypes.byref(tr), idx_base, ctypes.byref(te), k, num_classes, pred.data_ptr(),
             None if dist is None else dist.data_ptr(), None if idx is None else idx.data_ptr(),
-            None if stream is None else ctypes.c_void_p(stream))
+            _stream_arg(stream, test))
         if st != KNN_OK:
             raise KnnError(st, self.lib.knn_last_error(self.ctx.h).decode())
         return q0, q1

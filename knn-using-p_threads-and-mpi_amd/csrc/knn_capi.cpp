@@ -439,9 +439,9 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * (size_t)(d + 16) * nq));
         stage_begin(c, st, gate ? "aug_rerun" : "aug");
         HIP_OR_FAIL(c, knn_launch_aug_rows(tr->feat, dtype, ntp, nt, tr->ld, d, c->tnorm.as<float>(), 1.0f,
-                                           c->split_t.as<uint16_t>(), st, gate));
+                                           c->split_t.as<uint16_t>(), c->tmax.as<float4>(), st, gate));
         HIP_OR_FAIL(c, knn_launch_aug_rows(te->feat, dtype, nq, nq, te->ld, d, nullptr, -2.0f,
-                                           c->split_q.as<uint16_t>(), st, gate));
+                                           c->split_q.as<uint16_t>(), nullptr, st, gate));
         stage_end(c, st);
         ftrain = c->split_t.p; ftest = c->split_q.p;
         fld_t = fld_q = d + 16;
@@ -503,7 +503,6 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     g.coef = coef; g.eta = eta;
     g.gthr = c->gthr.as<uint32_t>();
     g.cnt = c->cnt.as<int32_t>(); g.cand = c->cand.as<CandRec>(); g.cap = cap; g.cap_seg = cap / nseg;
-    g.tstat = fused ? c->tmax.as<float4>() : nullptr;
     g.qstat = fused ? c->qstat.as<float2>() : nullptr;
     g.status = c->ctrl.as<int32_t>();
     g.gate = gate;

@@ -3,12 +3,22 @@
 // ordered-float bits, LDS-DMA issue and the GEMM filter tile geometry.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <float.h>
 #include <stdint.h>
 
 #include "knn_kernels.h"
 
 typedef unsigned long long u64;
+
+// Grid of a grid-stride elementwise kernel over `total` items (256 threads per block): at most
+// 2^20 blocks.  A dispatch's size is a 32-bit count of work-items, so one thread per item
+// would wrap for more than 2^32 items (a 32M x 256 generator fill has 8.2e9) and leave the
+// tail untouched.
+static inline unsigned elementwise_grid(int64_t total) {
+    return (unsigned)std::min<int64_t>((total + 255) / 256, (int64_t)1 << 20);
+}
 #define KNN_LAUNCH_CHECK() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return e_; } while (0)
 static constexpr u64 KEY_NONE = ~0ull;
 typedef float floatx16 __attribute__((ext_vector_type(16)));

@@ -2,8 +2,11 @@
 // folded into the MFMA (gfx950).  DESIGN.md "Fused-norm filter".
 //
 // Rows are augmented by 16 bf16 columns (k_aug_rows):
-//   train  [ rn(t_0) .. rn(t_{d-1}) | tn_hi tn_mid tn_lo 0 x 13 ]   (tn = ||t||^2, fp32)
+//   train  [ rn(t_0) .. rn(t_{d-1}) | tn_hi tn_mid tn_lo 0 x 5 | s0 s1 s2 0 x 5 ]   (tn = ||t||^2, fp32)
 //   query  [ -2 rn(q_0) .. -2 rn(q_{d-1}) | 1 1 1 0 x 13 ]
+// where s0..s2 (rows 32i only, else 0) are the 64-row tile's statistics {max tn, max |t - rt|,
+// max |rt|} rounded UP to bf16: they travel into LDS with the tile (no scalar loads in the
+// filter's loop) and multiply the queries' zero columns.
 // so one chain of v_mfma_f32_32x32x16_bf16 over d/16 + 1 k-steps leaves
 //   y = tn - 2 rn(q).rn(t)
 // in the accumulators: the fast test is a v_min3 chain over the 16 values of an
@@ -35,18 +38,29 @@ static constexpr int FUSED_RQ = 4;            // queued passing values per lane 
 // norms == NULL), then zeros.  One thread per 4 elements: a float4 (or 4 bf16) in, one
 // 8-byte bf16 quad out.
 // ---------------------------------------------------------------------------------
+// bf16 bits of the smallest bf16 >= x (x >= 0 finite): an upper bound stays one
+__device__ __forceinline__ uint32_t bf16_up(float x) {
+    const uint32_t b = __float_as_uint(x);
+    return (b >> 16) + ((b & 0xffffu) ? 1u : 0u);
+}
+
 template <typename E>
 __global__ __launch_bounds__(256) void k_aug_rows(const E* __restrict__ x, int64_t n, int64_t n_valid, int ld,
                                                   int d, const float* __restrict__ norms, float scale,
-                                                  bf16_t* __restrict__ out, const int32_t* __restrict__ gate) {
+                                                  bf16_t* __restrict__ out, const float4* __restrict__ tstat,
+                                                  const int32_t* __restrict__ gate) {
     if (gate && *gate == 0) return;
     const int per_row = (d + 16) >> 2;
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n * per_row) return;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n * per_row; i += (int64_t)gridDim.x * 256) {
     const int64_t r = i / per_row;
     const int c = (int)(i - r * per_row) * 4;
     uint32_t w0 = 0u, w1 = 0u;
-    if (r >= n_valid) {
+    if (c == d + 8 && tstat && (r & 31) == 0) {
+        // the 64-row tile's statistics (k_row_norms, over its valid rows), rounded up
+        const float4 t = tstat[r >> 6];
+        w0 = bf16_up(t.x) | (bf16_up(t.y) << 16);
+        w1 = bf16_up(t.z);
+    } else if (r >= n_valid) {
         // pad rows up to the 64-row tile grid (train only): zero features and tn_hi = 0x1.fep127,
         // so y = tn - 2 q.t ~ 1.7e38 never passes a fast test; their indices are past row_end
         if (c == d && norms) w0 = 0x7f7fu;
@@ -69,20 +83,21 @@ __global__ __launch_bounds__(256) void k_aug_rows(const E* __restrict__ x, int64
         }
     }
     *reinterpret_cast<uint2*>(out + r * (int64_t)(d + 16) + c) = make_uint2(w0, w1);
+    }
 }
 
 hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int64_t n_valid, int ld, int d, const float* norms,
-                               float scale, uint16_t* out, hipStream_t st, const int32_t* gate) {
+                               float scale, uint16_t* out, const float4* tstat, hipStream_t st, const int32_t* gate) {
     const int64_t total = n * ((d + 16) / 4);
     if (total <= 0) return hipSuccess;
     if (d % 4 || ld % 4) return hipErrorInvalidValue;
-    const dim3 grid((unsigned)((total + 255) / 256));
+    const dim3 grid(elementwise_grid(total));
     if (elem == ELEM_BF16)
         hipLaunchKernelGGL(k_aug_rows<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, n, n_valid, ld, d, norms, scale,
-                           (bf16_t*)out, gate);
+                           (bf16_t*)out, tstat, gate);
     else
         hipLaunchKernelGGL(k_aug_rows<float>, grid, dim3(256), 0, st, (const float*)x, n, n_valid, ld, d, norms, scale,
-                           (bf16_t*)out, gate);
+                           (bf16_t*)out, tstat, gate);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -184,18 +199,14 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         qe2 = 2.0f * qs.x * (1.0f + 0x1p-17f);
         eq2 = 2.0f * qs.y * (1.0f + 0x1p-17f);
     }
-    // the tile's stats by a scalar load (constant address space, wave-uniform index): counted
-    // by lgkmcnt, so using them never waits on the vector-memory count the tile DMAs share
-    auto tile_q = [&](int64_t tile) __attribute__((always_inline)) -> float2 {
-        const int ti = __builtin_amdgcn_readfirstlane((int)tile);
-#ifdef __HIP_DEVICE_COMPILE__
-        typedef __attribute__((address_space(4))) const float* cfloatp;
-        const cfloatp p = (cfloatp)(a.tstat + ti);
-        const float4 t = make_float4(p[0], p[1], p[2], p[3]);
-#else
-        const float4 t = a.tstat[ti];  // (the host pass only parses device code)
-#endif
-        return make_float2(t.x, fmaf(qe2, t.y, eq2 * t.z));
+    // the tile's statistics, from row 0 of its LDS image (augmented columns d+8..d+10, see
+    // k_aug_rows): one broadcast ds_read_b64, in order with the fragment reads -- no scalar
+    // memory load in the loop
+    auto tile_q = [&](int buf) __attribute__((always_inline)) -> float2 {
+        const uint2 w = *reinterpret_cast<const uint2*>(tiles + buf * TILE + (RB - 16));
+        const float tx = __uint_as_float(w.x << 16), ty = __uint_as_float(w.x & 0xffff0000u);
+        const float tz = __uint_as_float(w.y << 16);
+        return make_float2(tx, fmaf(qe2, ty, eq2 * tz));
     };
 
     const int ntiles = (row_end > row_begin) ? (int)((row_end - row_begin + BN - 1) / BN) : 0;
@@ -281,6 +292,10 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                 if (!KNN_STUDY_NO_EPI) {
 #pragma unroll
                     for (int v = s * VPS; v < (s + 1) * VPS && v < 16; v++) mn[c] = fminf(mn[c], Y[c][v]);
+                    // computed here, beside this k-step's MFMAs: without the opaque use the
+                    // compiler sinks the whole v_min3 chain into the last k-step, where it
+                    // runs exposed after the final MFMA
+                    if (s * VPS < 16) asm volatile("" : "+v"(mn[c]));
                 }
             }
             KNN_FUSED_KSTEP_ORDER();
@@ -539,9 +554,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         }
     constexpr bool DEFER = NW == 8 && !RL;
     // tile terms (max norm, rounding bound) of the tile in the pipeline (it) and of tile it-1
-    const int64_t tile0 = row_begin >> 6;
     float2 tm_prev = make_float2(0.0f, 0.0f);
-    float2 tmg[GRP];  // PAIR: the pair's tile terms, loaded after its barrier
     auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
         if ((it & (FUSED_SHARE_EVERY - 1)) == FUSED_SHARE_EVERY - 1) {
             if (a.nseg > 1 && qvalid) {
@@ -560,20 +573,9 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         // waits for all of its own vector-memory ops, then the barrier -- and every wave is done
         // with the buffers the next DMAs overwrite
         if (!PAIR || it % GRP == 0) wait_dma_barrier(0);
-        // this tile's terms, for its fast test in the next iteration: loaded after the barrier
-        float2 tm_cur;
-        if constexpr (PAIR) {
-            const int gi = it % GRP;
-            if (gi == 0) {
-#pragma unroll
-                for (int g = 0; g < GRP; g++) tmg[g] = tile_q(tile0 + ((min(it + g, ntiles - 1) * BN) >> 6));
-            }
-            tm_cur = tmg[0];
-#pragma unroll
-            for (int g = 1; g < GRP; g++) tm_cur = gi == g ? tmg[g] : tm_cur;
-        } else {
-            tm_cur = tile_q(tile0 + ((it * BN) >> 6));
-        }
+        // this tile's terms, for its fast test in the next iteration (the tile is resident:
+        // landed before this step's barrier, not overwritten before the next one)
+        const float2 tm_cur = tile_q(it % NBUF);
         const bool dma_on = !KNN_STUDY_NO_DMA && it + AHEAD < ntiles;
         const DmaTile dd = dma_desc((it + AHEAD) % NBUF, row_begin + (int64_t)(it + AHEAD) * BN);
         const float tf = it > 0 ? tf_of(tm_prev) : -INF;
@@ -764,7 +766,7 @@ hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu) {
 
 hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st) {
     const FilterPlan f = knn_fused_plan(a.d, a.k);
-    if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != a.d + 16 || a.ld_q != a.d + 16 || !a.tstat || !a.qstat)
+    if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != a.d + 16 || a.ld_q != a.d + 16 || !a.qstat)
         return hipErrorInvalidValue;
     if (f.kr > 0 && !(f.nw == 8 && f.rg == 2 && f.nbuf == 4)) return hipErrorInvalidValue;  // (fused_fn_k)
     void* args[] = {const_cast<GemmFilterArgs*>(&a)};

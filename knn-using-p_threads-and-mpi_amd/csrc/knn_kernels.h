@@ -52,7 +52,6 @@ struct GemmFilterArgs {
     uint32_t* gthr;
     int32_t* cnt;  // [nseg][nq] kept rows per (segment, query)
     CandRec* cand; int cap; int cap_seg;  // [nq][cap] candidate records
-    const float4* tstat;  // fused filter, per 64-row tile: {max tn, max |t - rt|, max |rt|, 0}
     const float2* qstat;  // fused filter, per query: {|q|, |q - rq|} upper bounds (rq: the operand / -2)
     // fused filter schedule (knn_fused_schedule): p1_blocks whole query tiles, then g2 blocks
     // over the remaining w2 (query tile, 64-row unit) pairs; tiles64 units per query tile
@@ -158,10 +157,12 @@ hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu);
 // a.seg_len / nseg instead: the segment schedule, n_qtiles * nseg blocks.)
 int knn_fused_schedule(GemmFilterArgs& a, int slots, int* nseg);
 hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st);
-// x [n_valid][ld] (fp32 or bf16) -> bf16 [n][d + 16]: rn(scale * x) | split of norms[r] (or 1 1 1) | 0;
+// x [n_valid][ld] (fp32 or bf16) -> bf16 [n][d + 16]: rn(scale * x) | split of norms[r] (or 1 1 1) | 0,
+// and (tstat != NULL, train) the 64-row tile statistics in columns d+8..d+10 of rows 32i;
 // rows n_valid .. n-1 (train: padding to the 64-row tile grid) never pass the filter
 hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int64_t n_valid, int ld, int d, const float* norms,
-                               float scale, uint16_t* out, hipStream_t st, const int32_t* gate = nullptr);
+                               float scale, uint16_t* out, const float4* tstat, hipStream_t st,
+                               const int32_t* gate = nullptr);
 hipError_t knn_launch_merge(const MergeArgs& a, hipStream_t st);
 hipError_t knn_launch_generate(const GenerateArgs& a, hipStream_t st);
 // the bf16 filter's MFMA chain on [32][K] bf16 operands (certificate self-test)

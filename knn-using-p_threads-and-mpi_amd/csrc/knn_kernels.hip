@@ -532,8 +532,7 @@ __global__ __launch_bounds__(256) void k_split_rows(const float* __restrict__ x,
                                                     bf16_t* __restrict__ out, const int32_t* __restrict__ gate) {
     if (gate && *gate == 0) return;
     const int per_row = d >> 2;
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n * per_row) return;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n * per_row; i += (int64_t)gridDim.x * 256) {
     const int64_t r = i / per_row;
     const int c = (int)(i - r * per_row) * 4;
     const float4 v = *reinterpret_cast<const float4*>(x + r * ld + c);
@@ -547,6 +546,7 @@ __global__ __launch_bounds__(256) void k_split_rows(const float* __restrict__ x,
     bf16_t* o = out + r * (int64_t)(2 * d) + c;
     *reinterpret_cast<uint2*>(o) = make_uint2(hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16));
     *reinterpret_cast<uint2*>(o + d) = make_uint2(lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16));
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -559,13 +559,13 @@ __global__ __launch_bounds__(256) void k_round_rows(const float* __restrict__ x,
                                                     bf16_t* __restrict__ out, const int32_t* __restrict__ gate) {
     if (gate && *gate == 0) return;
     const int per_row = d >> 2;
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n * per_row) return;
-    const int64_t r = i / per_row;
-    const int c = (int)(i - r * per_row) * 4;
-    const float4 v = *reinterpret_cast<const float4*>(x + r * ld + c);
-    *reinterpret_cast<uint2*>(out + r * (int64_t)d + c) =
-        make_uint2(bf16_rne(v.x) | (bf16_rne(v.y) << 16), bf16_rne(v.z) | (bf16_rne(v.w) << 16));
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n * per_row; i += (int64_t)gridDim.x * 256) {
+        const int64_t r = i / per_row;
+        const int c = (int)(i - r * per_row) * 4;
+        const float4 v = *reinterpret_cast<const float4*>(x + r * ld + c);
+        *reinterpret_cast<uint2*>(out + r * (int64_t)d + c) =
+            make_uint2(bf16_rne(v.x) | (bf16_rne(v.y) << 16), bf16_rne(v.z) | (bf16_rne(v.w) << 16));
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1439,8 +1439,8 @@ __device__ __forceinline__ uint64_t gen_hash(uint64_t seed, uint32_t stream, uin
 }
 
 __global__ __launch_bounds__(256) void k_generate(GenerateArgs a) {
-    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    int64_t total = a.n * a.ld;
+    const int64_t total = a.n * a.ld;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total || i < a.n; i += (int64_t)gridDim.x * 256) {
     if (i < total) {
         int64_t r = i / a.ld;
         int c = (int)(i % a.ld);
@@ -1458,6 +1458,7 @@ __global__ __launch_bounds__(256) void k_generate(GenerateArgs a) {
     if (a.labels && i < a.n) {
         uint32_t u = (uint32_t)(gen_hash(a.seed, a.stream, (uint64_t)(a.row0 + i), 0xFFFFu) >> 32);
         a.labels[i] = (int32_t)(u % (uint32_t)a.C);
+    }
     }
 }
 
@@ -1797,7 +1798,7 @@ hipError_t knn_launch_split_rows(const float* x, int64_t n, int ld, int d, uint1
     const int64_t total = n * (d / 4);
     if (total <= 0) return hipSuccess;
     if (d % 4 || ld % 4) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_split_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, n, ld, d, out, gate);
+    hipLaunchKernelGGL(k_split_rows, dim3(elementwise_grid(total)), dim3(256), 0, st, x, n, ld, d, out, gate);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -1807,7 +1808,7 @@ hipError_t knn_launch_round_rows(const float* x, int64_t n, int ld, int d, uint1
     const int64_t total = n * (d / 4);
     if (total <= 0) return hipSuccess;
     if (d % 4 || ld % 4) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_round_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, n, ld, d, out, gate);
+    hipLaunchKernelGGL(k_round_rows, dim3(elementwise_grid(total)), dim3(256), 0, st, x, n, ld, d, out, gate);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -1815,7 +1816,7 @@ hipError_t knn_launch_round_rows(const float* x, int64_t n, int ld, int d, uint1
 hipError_t knn_launch_generate(const GenerateArgs& a, hipStream_t st) {
     int64_t total = a.n * a.ld;
     if (total <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_generate, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_generate, dim3(elementwise_grid(std::max(total, a.n))), dim3(256), 0, st, a);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }
