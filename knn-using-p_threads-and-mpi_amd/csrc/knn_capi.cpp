@@ -435,10 +435,12 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     if (fused) {
         // augmented bf16 rows: train [rn(t) | tn split], queries [-2 rn(q) | 1 1 1]
         // (pad rows: zero features, a huge norm -- they never pass)
-        HIP_OR_FAIL(c, c->split_t.ensure(sizeof(uint16_t) * (size_t)(d + 16) * ntp));
+        // (one more tile of pad rows past the grid: the filter scans tiles in twos, k_gemm_fused)
+        const int64_t ntf = ntp + 64;
+        HIP_OR_FAIL(c, c->split_t.ensure(sizeof(uint16_t) * (size_t)(d + 16) * ntf));
         HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * (size_t)(d + 16) * nq));
         stage_begin(c, st, gate ? "aug_rerun" : "aug");
-        HIP_OR_FAIL(c, knn_launch_aug_rows(tr->feat, dtype, ntp, nt, tr->ld, d, c->tnorm.as<float>(), 1.0f,
+        HIP_OR_FAIL(c, knn_launch_aug_rows(tr->feat, dtype, ntf, nt, tr->ld, d, c->tnorm.as<float>(), 1.0f,
                                            c->split_t.as<uint16_t>(), c->tmax.as<float4>(), st, gate));
         HIP_OR_FAIL(c, knn_launch_aug_rows(te->feat, dtype, nq, nq, te->ld, d, nullptr, -2.0f,
                                            c->split_q.as<uint16_t>(), nullptr, st, gate));

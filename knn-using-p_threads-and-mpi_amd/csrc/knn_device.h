@@ -250,17 +250,18 @@ __device__ __forceinline__ void dma4s(uint32_t voff, const void* sbase, uint32_t
                  : "v"(voff), "s"(sbase), "s"(lds)
                  : "memory");
 }
-// wait until at most n (wave-uniform, <= 15) vector-memory ops of this wave are in
-// flight, then barrier: vmcnt retires in issue order for loads (the DMAs)
-__device__ __forceinline__ void wait_dma_barrier(int n) {
-#define KNN_WAIT_CASE(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")\n\ts_barrier" ::: "memory"); break;
-    switch (n) {
-        KNN_WAIT_CASE(1) KNN_WAIT_CASE(2) KNN_WAIT_CASE(3) KNN_WAIT_CASE(4) KNN_WAIT_CASE(5)
-        KNN_WAIT_CASE(6) KNN_WAIT_CASE(7) KNN_WAIT_CASE(8) KNN_WAIT_CASE(9) KNN_WAIT_CASE(10)
-        KNN_WAIT_CASE(11) KNN_WAIT_CASE(12) KNN_WAIT_CASE(13) KNN_WAIT_CASE(14) KNN_WAIT_CASE(15)
-        default: asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory"); break;
-    }
-#undef KNN_WAIT_CASE
+// The tile barrier of the LDS-DMA filters: this wave's tile DMAs have landed (vmcnt(0): its
+// pieces of the tiles about to be read) AND every LDS read it issued has returned its data
+// (lgkmcnt(0)), then s_barrier.  Both halves are needed:
+//  * RAW -- after the barrier every wave's pieces of the next tiles are in LDS;
+//  * WAR -- a ds_read is asynchronous, and s_barrier does not wait for it.  The DMAs issued
+//    after this barrier overwrite the buffers the previous tiles used; a read of such a buffer
+//    still in flight at the barrier (its MFMA scheduled after it) would return the NEW bytes.
+//    With lgkmcnt(0) here no read of any earlier tile outlives the barrier, whatever order
+//    the compiler gives the k-steps (without it the filter was correct only while a
+//    per-k-step sched_barrier kept each tile's reads and MFMAs ahead of the barrier).
+__device__ __forceinline__ void wait_dma_barrier() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // per-query 4-ary heap stride in floats: node n >= 1 in slot n-1, the root in the last slot;

@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void k_aug_rows(const E* __restrict__ x, int64
     const int64_t r = i / per_row;
     const int c = (int)(i - r * per_row) * 4;
     uint32_t w0 = 0u, w1 = 0u;
-    if (c == d + 8 && tstat && (r & 31) == 0) {
+    if (c == d + 8 && tstat && (r & 31) == 0 && (r >> 6) < (n_valid + 63) >> 6) {
         // the 64-row tile's statistics (k_row_norms, over its valid rows), rounded up
         const float4 t = tstat[r >> 6];
         w0 = bf16_up(t.x) | (bf16_up(t.y) << 16);
@@ -141,10 +141,11 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     constexpr bool PAIR = GRP > 1;
     constexpr int AHEAD = PAIR ? GRP : NBUF - 1;  // tiles between a step and the tile it DMAs
     static_assert(RG == 1 || RG == 2, "row groups");
-    static_assert(KR == 0 || KR == 16 || KR == 32, "register lists: k <= 16, k <= 32, or LDS heaps");
-    constexpr bool RL = KR > 0;       // thresholds from per-lane register lists (else LDS heaps)
-    constexpr bool HALVES = KR == 32;  // k <= 32: one 16-entry list per lane half (below)
-    constexpr int LL = 16;             // register list length
+    static_assert(KR == 0 || KR == 8 || KR == 16 || KR == 32,
+                  "register lists: k <= 16 (shared 16 or per-half 8 entries), k <= 32, or LDS heaps");
+    constexpr bool RL = KR > 0;                   // thresholds from per-lane register lists (else LDS heaps)
+    constexpr bool HALVES = KR == 32 || KR == 8;  // one list per lane half (below): k <= 2 LL
+    constexpr int LL = KR == 8 ? 8 : 16;          // register list length
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* tiles = smem;                                     // [NBUF][TILE]
     const int hs = heap_stride(a.k);
@@ -209,7 +210,12 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         return make_float2(tx, fmaf(qe2, ty, eq2 * tz));
     };
 
-    const int ntiles = (row_end > row_begin) ? (int)((row_end - row_begin + BN - 1) / BN) : 0;
+    // tiles of the piece, rounded up to an even count: the scan loop below runs tiles in twos
+    // with no exit between them, so only accB is live out of it (with an odd tail the compiler
+    // copies both accumulator sets -- 32 v_mov -- at every back edge).  The extra tile reads the
+    // next 64 rows (another piece's, or the padding the augmented train rows carry past the
+    // tile grid, run_gemm), which the row_end test rejects.
+    const int ntiles = (row_end > row_begin) ? ((int)((row_end - row_begin + BN - 1) / BN) + 1) & ~1 : 0;
 
     // ---- LDS-DMA of tiles (same image as k_gemm_filter: slot P -> row P / SLOTS, slot P % SLOTS,
     // the pad slot duplicates slot 0; rows past row_end are read (padding or the next piece's
@@ -432,8 +438,9 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // their candidate U (v_permlane32_swap) and both insert both (32 v_med3, the multiset and
     // so the list come out the same in either order): the query's exact k-th smallest, like
     // the heap, for all 32 queries of the wave at once -- no LDS, no lane takes turns.
-    // HALVES (16 < k <= 32): each lane keeps its own half's ceil(k/2) smallest U (16 - ceil(k/2)
-    // pads) and inserts only its own values (16 v_med3); the bound is the larger of the two
+    // HALVES (16 < k <= 32, KR = 32; KR = 8: k <= 16 with 8-entry lists): each lane keeps its own
+    // half's ceil(k/2) smallest U (LL - ceil(k/2) pads) and inserts only its own values (LL
+    // v_med3); the bound is the larger of the two
     // halves' ceil(k/2)-th smallest -- at least 2 ceil(k/2) >= k kept rows have U <= it.  A
     // little looser than the exact k-th smallest, with no LDS heap and no turn-taking.
     float lst[RL ? LL : 1];
@@ -572,7 +579,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         // the tiles of this step (both of a pair) have landed -- every wave's pieces: each wave
         // waits for all of its own vector-memory ops, then the barrier -- and every wave is done
         // with the buffers the next DMAs overwrite
-        if (!PAIR || it % GRP == 0) wait_dma_barrier(0);
+        if (!PAIR || it % GRP == 0) wait_dma_barrier();
         // this tile's terms, for its fast test in the next iteration (the tile is resident:
         // landed before this step's barrier, not overwritten before the next one)
         const float2 tm_cur = tile_q(it % NBUF);
@@ -599,21 +606,17 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     };
     for (int it = 0; it < ntiles; it += 2) {
         iter(accA, accB, it);
-        if (it + 1 < ntiles) iter(accB, accA, it + 1);
+        iter(accB, accA, it + 1);
     }
     if (ntiles > 0) {
-        // drain: the last tile's accumulators are in accA (ntiles odd) or accB (even)
+        // drain: the last tile's accumulators (ntiles is even: accB)
         const int last = ntiles - 1;
-        auto drain = [&](floatx16 (&Lc)[NACC]) {
-            const float tf = tf_of(tm_prev);
-            if (pass_set(Lc, tf, 0xffffffffu)) {
-                if constexpr (RL) slow_rl(Lc, last, tf, tm_prev, 0xffffffffu);
-                else if constexpr (DEFER) record(Lc, last, tf, tm_prev, 0xffffffffu);
-                else slow(Lc, last, tf, tm_prev, 0xffffffffu);
-            }
-        };
-        if (last & 1) drain(accB);
-        else drain(accA);
+        const float tf = tf_of(tm_prev);
+        if (pass_set(accB, tf, 0xffffffffu)) {
+            if constexpr (RL) slow_rl(accB, last, tf, tm_prev, 0xffffffffu);
+            else if constexpr (DEFER) record(accB, last, tf, tm_prev, 0xffffffffu);
+            else slow(accB, last, tf, tm_prev, 0xffffffffu);
+        }
     }
     if constexpr (DEFER) {
         if (__ballot(qcnt > 0)) flush();
@@ -724,7 +727,7 @@ bool knn_fused_supported(int d) { return d == 64 || d == 128 || d == 256; }
 FilterPlan knn_fused_plan(int d, int k) {
     const int rb = 2 * d + 32;
     const size_t cap = 160 * 1024 - 256;  // room for the kernel's static LDS
-    const int kr = k <= 16 ? 16 : k <= 32 ? 32 : 0;
+    const int kr = k <= 16 ? KNN_FUSED_SMALL_K_LIST : k <= 32 ? 32 : 0;
     auto make = [&](int nw, int rg, int minw, int nbuf) {
         FilterPlan f{nw, 0, rg, minw, nbuf, 32 * nw, fused_lds_of(rb, k, nw, rg, nbuf, kr == 0)};
         f.kr = kr;
@@ -751,7 +754,8 @@ static const void* fused_fn_k(const FilterPlan& f) {
 }
 template <int RB>
 static const void* fused_fn(const FilterPlan& f) {
-    return f.kr == 16 ? fused_fn_k<RB, 16>(f) : f.kr == 32 ? fused_fn_k<RB, 32>(f) : fused_fn_k<RB, 0>(f);
+    return f.kr == 16 ? fused_fn_k<RB, 16>(f) : f.kr == 8 ? fused_fn_k<RB, 8>(f) : f.kr == 32 ? fused_fn_k<RB, 32>(f)
+                                                                                   : fused_fn_k<RB, 0>(f);
 }
 
 static const void* fused_ptr(int d, const FilterPlan& f) {

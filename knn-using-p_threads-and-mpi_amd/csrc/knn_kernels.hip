@@ -1037,7 +1037,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
         }
         // tile it landed; every wave is done with the buffer / ring slot the next DMA
         // overwrites (tile it-1's, read last iteration)
-        wait_dma_barrier(0);
+        wait_dma_barrier();
         const bool dma_on = !KNN_STUDY_NO_DMA && it + NBUF - 1 < ntiles;
         const DmaTile dd = dma_desc((it + NBUF - 1) % NBUF, (it + NBUF - 1) % NR, r0 + (int64_t)(NBUF - 1) * BN);
         const bool any = step(X, Y, it % NBUF, (it + NR - 1) % NR, dma_on, dd);

@@ -40,12 +40,23 @@
 
 // The fused filter's instruction order inside a k-step (knn_fused.hip, step()): a full
 // scheduling barrier after every k-step keeps each step's A-fragment prefetch, DMA piece,
-// MFMAs and fast-test VALU together.  KNN_FUSED_FREE_SCHEDULE (study) lets the compiler
-// schedule across the steps.
+// MFMAs and fast-test VALU together -- a performance choice only: correctness rests on the
+// tile barrier retiring every LDS read (wait_dma_barrier), and the free schedule passes the
+// parity suite.  KNN_FUSED_FREE_SCHEDULE (study) lets the compiler schedule across
+// the steps.
 #ifdef KNN_FUSED_FREE_SCHEDULE
 #define KNN_FUSED_KSTEP_ORDER() \
     do {                        \
     } while (0)
 #else
 #define KNN_FUSED_KSTEP_ORDER() __builtin_amdgcn_sched_barrier(0)
+#endif
+
+// Register lists for k <= 16 (knn_fused_plan): 16 = one exact list per query shared by its two
+// lanes (both insert both values); 8 = the per-half lists of k <= 32 with 8 entries (each lane
+// inserts only its own value; a looser bound).  KNN_STUDY_HALF_LISTS selects 8.
+#ifdef KNN_STUDY_HALF_LISTS
+#define KNN_FUSED_SMALL_K_LIST 8
+#else
+#define KNN_FUSED_SMALL_K_LIST 16
 #endif

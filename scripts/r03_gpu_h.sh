@@ -1,0 +1,18 @@
+#!/bin/bash
+# round 3, pass h: baseline of HEAD -- the whole GPU suite (config C at size included), then
+# bench lines A (with the CPU baseline), B and C1 (with the CPU baseline at d=256, k=100).
+set -o pipefail
+mkdir -p gpurun_out
+P=r03h
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 500 --timeout-method thread --durations=15 \
+  > gpurun_out/${P}_pytest_gpu.log 2>&1
+rc=$?
+echo "suite rc=$rc :: $(tail -1 gpurun_out/${P}_pytest_gpu.log)"; grep -E '^FAILED|^ERROR' gpurun_out/${P}_pytest_gpu.log | head
+[ $rc -ne 0 ] && exit 1
+timeout -k 10 300 python -u bench.py --config A --steps 20 --warmup 3 > gpurun_out/${P}_bench_A.log 2>&1 || { echo "bench A failed"; tail -5 gpurun_out/${P}_bench_A.log; exit 1; }
+echo "A: $(tail -1 gpurun_out/${P}_bench_A.log | cut -c1-300)"
+timeout -k 10 300 python -u bench.py --config B --steps 2 --warmup 1 --no-cpu-baseline --no-host-path > gpurun_out/${P}_bench_B.log 2>&1 || { echo "bench B failed"; tail -5 gpurun_out/${P}_bench_B.log; exit 1; }
+echo "B: $(tail -1 gpurun_out/${P}_bench_B.log | cut -c1-300)"
+timeout -k 10 400 python -u bench.py --config C1 --steps 2 --warmup 1 > gpurun_out/${P}_bench_C1.log 2>&1 || { echo "bench C1 failed"; tail -5 gpurun_out/${P}_bench_C1.log; exit 1; }
+echo "C1: $(tail -1 gpurun_out/${P}_bench_C1.log | cut -c1-300)"
+echo done
