@@ -134,10 +134,11 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     constexpr int DMA_PER_WAVE = (DMA_INS + NW - 1) / NW;
     constexpr int NS = RB / 32;                  // k-steps: d/16 feature steps + the norm step
     constexpr int VPS = (16 + NS - 1) / NS;      // fast-test values per k-step per accumulator
-    static_assert(NBUF == 2 || NBUF == 4, "tile buffers: two, or four (tiles in pairs)");
+    static_assert(NBUF == 2 || NBUF == 4 || NBUF == 8, "tile buffers: two, four (tiles in pairs) or eight (quads)");
     // NBUF = 4: tiles go in pairs -- one barrier per pair; the DMA of tile it + 2 is issued
     // during step it into the buffer tile it - 2 used (read before this pair's barrier)
-    constexpr int GRP = NBUF == 4 ? 2 : 1;
+    // (NBUF = 8: groups of four tiles, one barrier per four, DMA four tiles ahead)
+    constexpr int GRP = NBUF >= 4 ? NBUF / 2 : 1;
     constexpr bool PAIR = GRP > 1;
     constexpr int AHEAD = PAIR ? GRP : NBUF - 1;  // tiles between a step and the tile it DMAs
     static_assert(RG == 1 || RG == 2, "row groups");
@@ -734,6 +735,7 @@ FilterPlan knn_fused_plan(int d, int k) {
         return f;
     };
     if (kr == 0 && d == 64 && fused_lds_of(rb, k, 4, 2, 2, true) <= cap / 2) return make(4, 2, 2, 2);
+    if (KNN_FUSED_QUADS && kr > 0 && fused_lds_of(rb, k, 8, 2, 8, false) <= cap) return make(8, 2, 2, 8);
     if (fused_lds_of(rb, k, 8, 2, 4, kr == 0) <= cap) return make(8, 2, 2, 4);
     if (fused_lds_of(rb, k, 8, 2, 2, kr == 0) <= cap) return make(8, 2, 2, 2);
     if (fused_lds_of(rb, k, 8, 1, 2, kr == 0) <= cap) return make(8, 1, 2, 2);
@@ -744,6 +746,9 @@ template <int RB, int KR>
 static const void* fused_fn_k(const FilterPlan& f) {
 #define KNN_FUSED_FN(NB, NW, RG) reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, NB, NW, RG, KR>)
     if constexpr (KR > 0) {
+        if constexpr (KNN_FUSED_QUADS) {
+            if (f.nbuf == 8) return KNN_FUSED_FN(8, 8, 2);
+        }
         return KNN_FUSED_FN(4, 8, 2);  // register lists always fit the pairs shape
     } else {
         if (f.nw == 4) return KNN_FUSED_FN(2, 4, 2);
@@ -772,7 +777,8 @@ hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st) {
     const FilterPlan f = knn_fused_plan(a.d, a.k);
     if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != a.d + 16 || a.ld_q != a.d + 16 || !a.qstat)
         return hipErrorInvalidValue;
-    if (f.kr > 0 && !(f.nw == 8 && f.rg == 2 && f.nbuf == 4)) return hipErrorInvalidValue;  // (fused_fn_k)
+    if (f.kr > 0 && !(f.nw == 8 && f.rg == 2 && (f.nbuf == 4 || (KNN_FUSED_QUADS && f.nbuf == 8))))
+        return hipErrorInvalidValue;  // (fused_fn_k)
     void* args[] = {const_cast<GemmFilterArgs*>(&a)};
     const dim3 grid((unsigned)(a.g2 < 0 ? (int64_t)a.n_qtiles * a.nseg : (int64_t)a.p1_blocks + a.g2));
     hipError_t e = hipLaunchKernel(fused_ptr(a.d, f), grid, dim3(64 * f.nw), args, f.lds, st);

@@ -60,3 +60,12 @@
 #else
 #define KNN_FUSED_SMALL_K_LIST 16
 #endif
+
+// Tile groups of the register-list shapes (knn_fused_plan): pairs (four buffers, one barrier per
+// two tiles); KNN_STUDY_QUADS: quads where the LDS holds eight buffers (d <= 128), one barrier
+// per four tiles.
+#ifdef KNN_STUDY_QUADS
+#define KNN_FUSED_QUADS 1
+#else
+#define KNN_FUSED_QUADS 0
+#endif
