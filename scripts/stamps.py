@@ -1,0 +1,40 @@
+"""Timing study (KNN_AMD_LIB=.../build/ablate/libknn_amd_stamps.so): where a fused-filter
+wave's cycles go on configs A and B -- barrier wait, step (MFMAs + fast test + DMA issue),
+slow path -- from the per-wave shader-clock stamps of the KNN_STUDY_STAMPS build
+(knn_fused.hip).  Prints one line per config."""
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+from conftest import load_pkg  # noqa: E402
+
+knn = load_pkg()
+lib = knn.load_library()
+lib.knn_debug_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+buf = (ctypes.c_ulonglong * 8)()
+dev = torch.device("cuda", 0)
+for name, nt, nq, d, k, seed in [("A", 1_000_000, 100_000, 128, 10, 1), ("B", 4_000_000, 1_000_000, 64, 32, 2)]:
+    ctx = knn.Context(0, algo="auto", profile=True)
+    train = torch.empty((nt, d), dtype=torch.float32, device=dev)
+    labels = torch.empty(nt, dtype=torch.int32, device=dev)
+    test = torch.empty((nq, d), dtype=torch.float32, device=dev)
+    ctx.generate(train, labels, 0, d, 0, seed, 0, 10)
+    ctx.generate(test, None, 0, d, 0, seed, 1, 10)
+    pred = torch.empty(nq, dtype=torch.int32, device=dev)
+    ctx.predict_device(train, labels, test, k, 10, pred)
+    torch.cuda.synchronize()
+    lib.knn_debug_stamps(buf, 1)
+    ctx.predict_device(train, labels, test, k, 10, pred)
+    torch.cuda.synchronize()
+    st = ctx.stage_times()
+    lib.knn_debug_stamps(buf, 1)
+    bar, step, slow, piece, slow_tiles, tiles, waves = (int(buf[i]) for i in range(7))
+    print(f"{name}: filter {st.get('gemm_filter', 0):.2f} ms; per wave-piece sums over {waves} wave-pieces: "
+          f"barrier {bar / piece:.3f}, step {step / piece:.3f}, slow {slow / piece:.3f} of the piece cycles; "
+          f"tiles with a slow path {slow_tiles / tiles:.3f}; slow cycles per such tile {slow / max(slow_tiles, 1):.0f}; "
+          f"step cycles per tile {step / tiles:.0f}; barrier cycles per tile {bar / tiles:.0f}", flush=True)
+    ctx.close()
+    del train, labels, test, pred
