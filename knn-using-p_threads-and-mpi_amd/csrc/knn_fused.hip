@@ -124,6 +124,20 @@ hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int64_t n_val
 // ---------------------------------------------------------------------------------
 // fused_piece: one piece of work -- query tile qt against train rows [row_begin, row_end),
 // piece (segment) id seg of that query tile (its candidate sub-slices, 2 seg + h)
+#if KNN_FUSED_STAMPS
+// per-wave sums over the launch: barrier wait, step, slow path, piece cycles, tiles with a
+// slow path, tiles, pieces (read by knn_debug_stamps; study build only)
+__device__ unsigned long long g_knn_stamps[8];
+extern "C" int knn_debug_stamps(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_knn_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_knn_stamps), zero, sizeof(zero)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
+
 template <int RB, int NBUF, int NW, int RG, int KR>
 __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int qt, const int seg,
                                             const int64_t row_begin, const int64_t row_end) {
@@ -134,13 +148,17 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     constexpr int DMA_PER_WAVE = (DMA_INS + NW - 1) / NW;
     constexpr int NS = RB / 32;                  // k-steps: d/16 feature steps + the norm step
     constexpr int VPS = (16 + NS - 1) / NS;      // fast-test values per k-step per accumulator
-    static_assert(NBUF == 2 || NBUF == 4 || NBUF == 8, "tile buffers: two, four (tiles in pairs) or eight (quads)");
+    static_assert(NBUF == 2 || NBUF == 4 || NBUF == 6 || NBUF == 8,
+                  "tile buffers: two, four (tiles in pairs), six (pairs, DMA two pairs ahead) or eight (quads)");
     // NBUF = 4: tiles go in pairs -- one barrier per pair; the DMA of tile it + 2 is issued
     // during step it into the buffer tile it - 2 used (read before this pair's barrier)
-    // (NBUF = 8: groups of four tiles, one barrier per four, DMA four tiles ahead)
-    constexpr int GRP = NBUF >= 4 ? NBUF / 2 : 1;
+    // (NBUF = 8: groups of four tiles, one barrier per four, DMA four tiles ahead; NBUF = 6:
+    // pairs with the DMA two pairs ahead -- a pair's barrier waits only for its own tiles'
+    // pieces, the next pair's stay in flight: vmcnt(pieces issued since))
+    constexpr int GRP = NBUF == 8 ? 4 : NBUF >= 4 ? 2 : 1;
     constexpr bool PAIR = GRP > 1;
-    constexpr int AHEAD = PAIR ? GRP : NBUF - 1;  // tiles between a step and the tile it DMAs
+    constexpr bool DEEP = NBUF == 6;
+    constexpr int AHEAD = DEEP ? 4 : PAIR ? GRP : NBUF - 1;  // tiles between a step and the tile it DMAs
     static_assert(RG == 1 || RG == 2, "row groups");
     static_assert(KR == 0 || KR == 8 || KR == 16 || KR == 32,
                   "register lists: k <= 16 (shared 16 or per-half 8 entries), k <= 32, or LDS heaps");
@@ -242,6 +260,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             dma16s(doff[i], d.src, d.lds + (uint32_t)ins * 1024u);
         }
     };
+    const int npw = (DMA_INS - wave + NW - 1) / NW;  // DMA instructions this wave issues per tile
     // piece i goes out in k-step (i NS) / DMA_PER_WAVE of the step
     auto dma_at = [&](int s, bool on, const DmaTile& d) __attribute__((always_inline)) {
 #pragma unroll
@@ -460,20 +479,61 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     auto partner = [&](float x) __attribute__((always_inline)) -> float {
         return __uint_as_float(lane_xor(__float_as_uint(x), 32));
     };
+    // Lane-parallel slow path.  Passes are sparse (A: a wave-tile has one in about 8 tiles,
+    // usually one query, one value), so instead of visiting the passing positions one
+    // wave-wide step at a time, every lane takes ITS OWN passing values, one per round, all
+    // lanes at once: a scan of the lane's 16 values of a passing accumulator (v_cmp + selects
+    // per value) yields the highest passing index below the previous round's, its value and
+    // (first round) how many pass; fn(c, idx, y) then handles every lane's candidate together
+    // (idx < 0: none).  Rounds = the most passing values of one lane in the accumulator (1
+    // unless the threshold is still loose).  Any processing order keeps every true neighbour:
+    // a row is kept iff L <= the threshold at its turn, and the threshold is always the k-th
+    // smallest U of kept rows.
+    auto lane_rounds = [&](floatx16 (&Y)[NACC], float tf, uint32_t u, auto&& fn) __attribute__((always_inline)) {
+#pragma unroll
+        for (int c = 0; c < NACC; c++) {
+            if (!((u >> (16 * c)) & 1u)) continue;  // (wave-uniform) no lane passes in c
+            // round 1: the highest passing index, its value, the lane's passing count
+            int idx = -1, cnt = 0;
+            float yv = INF;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const bool p = Y[c][r] <= tf;
+                idx = p ? r : idx;
+                yv = p ? Y[c][r] : yv;
+                cnt += p ? 1 : 0;
+            }
+            fn(c, idx, yv);
+            // further rounds (some lane has more passing values): the highest passing index
+            // below the last one taken
+            if (__ballot(cnt > 1)) {
+                int lim = idx;
+#pragma unroll 1
+                for (int round = 1; round < 16; round++) {
+                    idx = -1;
+                    yv = INF;
+#pragma unroll
+                    for (int r = 0; r < 16; r++) {
+                        const bool p = Y[c][r] <= tf && r < lim;
+                        idx = p ? r : idx;
+                        yv = p ? Y[c][r] : yv;
+                    }
+                    if (!__ballot(idx >= 0)) break;
+                    fn(c, idx, yv);
+                    lim = idx;
+                }
+            }
+        }
+    };
     auto slow_rl = [&](floatx16 (&Y)[NACC], int tp, float tf, float2 tq, uint32_t u) {
         if constexpr (RL) {
             const int64_t tbase = row_begin + (int64_t)tp * BN;
-            u = pass_set(Y, tf, u);
-            while (u) {
-                const int v = __builtin_ctz(u);
-                u &= u - 1u;
-                const float y = yval(Y, v);
-                const int r = v & 15;
-                const int row = 32 * (v >> 4) + (r & 3) + 8 * (r >> 2) + 4 * h;
+            auto visit = [&](int c, int idx, float yv) __attribute__((always_inline)) {
+                const int row = 32 * c + (idx & 3) + 8 * (idx >> 2) + 4 * h;
                 const int64_t t = tbase + row;
                 float L, U;
-                bounds(y, tq, L, U);
-                const bool keep = y <= tf && t < row_end && L <= thr;
+                bounds(yv, tq, L, U);
+                const bool keep = idx >= 0 && t < row_end && L <= thr;
                 if (keep) store_cand(L, U, t);
                 const float w = (keep && U < lst[LL - 1]) ? U : INF;
                 if constexpr (HALVES) {
@@ -490,7 +550,8 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                         thr = fminf(thr, lst[LL - 1]);
                     }
                 }
-            }
+            };
+            lane_rounds(Y, tf, u, visit);
             make_tfb();
         }
     };
@@ -523,30 +584,22 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     };
     auto record = [&](floatx16 (&Y)[NACC], int tp, float tf, float2 tq, uint32_t u) {
         const int64_t tbase = row_begin + (int64_t)tp * BN;
-        u = pass_set(Y, tf, u);
-        while (u) {
-            const int v = __builtin_ctz(u);
-            u &= u - 1u;
-            const float y = yval(Y, v);
-            const bool p = y <= tf;
-            if (__ballot(p && qcnt >= RQ)) flush();
-            const int r = v & 15;
-            const int row = 32 * (v >> 4) + (r & 3) + 8 * (r >> 2) + 4 * h;
+        lane_rounds(Y, tf, u, [&](int c, int idx, float yv) __attribute__((always_inline)) {
+            if (__ballot(idx >= 0 && qcnt >= RQ)) flush();
+            const int row = 32 * c + (idx & 3) + 8 * (idx >> 2) + 4 * h;
             const int64_t t = tbase + row;
-            if (p && t < row_end) {
-                float L, U;
-                bounds(y, tq, L, U);
-                if (L <= thr) {
+            float L, U;
+            bounds(yv, tq, L, U);
+            if (idx >= 0 && t < row_end && L <= thr) {
 #pragma unroll
-                    for (int i = 0; i < RQ; i++) {
-                        qL[i] = i == qcnt ? L : qL[i];
-                        qU[i] = i == qcnt ? U : qU[i];
-                        qT[i] = i == qcnt ? (int)t : qT[i];
-                    }
-                    qcnt++;
+                for (int i = 0; i < RQ; i++) {
+                    qL[i] = i == qcnt ? L : qL[i];
+                    qU[i] = i == qcnt ? U : qU[i];
+                    qT[i] = i == qcnt ? (int)t : qT[i];
                 }
+                qcnt++;
             }
-        }
+        });
     };
 
     floatx16 accA[NACC], accB[NACC];
@@ -563,6 +616,12 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     constexpr bool DEFER = NW == 8 && !RL;
     // tile terms (max norm, rounding bound) of the tile in the pipeline (it) and of tile it-1
     float2 tm_prev = make_float2(0.0f, 0.0f);
+    // study build KNN_STUDY_STAMPS: shader-clock stamps per wave (barrier wait, step, slow path)
+    uint64_t st_bar = 0, st_step = 0, st_slow = 0, st_visits = 0;
+    const uint64_t st_start = KNN_FUSED_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    auto now = [&]() __attribute__((always_inline)) -> uint64_t {
+        return KNN_FUSED_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    };
     auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
         if ((it & (FUSED_SHARE_EVERY - 1)) == FUSED_SHARE_EVERY - 1) {
             if (a.nseg > 1 && qvalid) {
@@ -580,7 +639,16 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         // the tiles of this step (both of a pair) have landed -- every wave's pieces: each wave
         // waits for all of its own vector-memory ops, then the barrier -- and every wave is done
         // with the buffers the next DMAs overwrite
-        if (!PAIR || it % GRP == 0) wait_dma_barrier();
+        const uint64_t t0 = now();
+        if constexpr (DEEP) {
+            // this wave's pieces of tiles it + 2, it + 3 (DMA'd during the previous pair, or by
+            // the prologue) may stay in flight; everything older -- this pair's tiles -- lands
+            if (it % GRP == 0)
+                wait_dma_barrier_n(npw * ((it + 2 < ntiles ? 1 : 0) + (it + 3 < ntiles ? 1 : 0)));
+        } else {
+            if (!PAIR || it % GRP == 0) wait_dma_barrier();
+        }
+        const uint64_t t1 = now();
         // this tile's terms, for its fast test in the next iteration (the tile is resident:
         // landed before this step's barrier, not overwritten before the next one)
         const float2 tm_cur = tile_q(it % NBUF);
@@ -591,6 +659,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         // PAIR: the pair's next tile is resident since its barrier -- its first fragments are
         // read now, so their latency hides under the slow path below
         if (PAIR && it % GRP != GRP - 1 && it + 1 < ntiles) prefetch((it + 1) % NBUF);
+        const uint64_t t2 = now();
         if (!KNN_STUDY_NO_SLOW) {
             if (uY) {
                 if constexpr (RL) slow_rl(Y, it - 1, tf, tm_prev, uY);
@@ -602,6 +671,13 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             }
         } else {
             asm volatile("" ::"s"(uY));
+        }
+        if constexpr (KNN_FUSED_STAMPS) {
+            const uint64_t t3 = now();
+            st_bar += t1 - t0;
+            st_step += t2 - t1;
+            st_slow += t3 - t2;
+            st_visits += uY ? 1 : 0;
         }
         tm_prev = tm_cur;
     };
@@ -628,6 +704,19 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
     if (qvalid) a.cnt[(int64_t)(2 * seg + h) * a.nq + q] = ccnt;
+#if KNN_FUSED_STAMPS
+    {
+        if (lane == 0) {
+            atomicAdd(&g_knn_stamps[0], (unsigned long long)st_bar);
+            atomicAdd(&g_knn_stamps[1], (unsigned long long)st_step);
+            atomicAdd(&g_knn_stamps[2], (unsigned long long)st_slow);
+            atomicAdd(&g_knn_stamps[3], (unsigned long long)(now() - st_start));
+            atomicAdd(&g_knn_stamps[4], (unsigned long long)st_visits);
+            atomicAdd(&g_knn_stamps[5], (unsigned long long)ntiles);
+            atomicAdd(&g_knn_stamps[6], 1ull);
+        }
+    }
+#endif
 }
 
 // The grid (knn_fused_schedule): blocks [0, p1) take one whole query tile each (qt = block,
@@ -736,6 +825,7 @@ FilterPlan knn_fused_plan(int d, int k) {
     };
     if (kr == 0 && d == 64 && fused_lds_of(rb, k, 4, 2, 2, true) <= cap / 2) return make(4, 2, 2, 2);
     if (KNN_FUSED_QUADS && kr > 0 && fused_lds_of(rb, k, 8, 2, 8, false) <= cap) return make(8, 2, 2, 8);
+    if (KNN_FUSED_DEEP && kr > 0 && fused_lds_of(rb, k, 8, 2, 6, false) <= cap) return make(8, 2, 2, 6);
     if (fused_lds_of(rb, k, 8, 2, 4, kr == 0) <= cap) return make(8, 2, 2, 4);
     if (fused_lds_of(rb, k, 8, 2, 2, kr == 0) <= cap) return make(8, 2, 2, 2);
     if (fused_lds_of(rb, k, 8, 1, 2, kr == 0) <= cap) return make(8, 1, 2, 2);
@@ -748,6 +838,9 @@ static const void* fused_fn_k(const FilterPlan& f) {
     if constexpr (KR > 0) {
         if constexpr (KNN_FUSED_QUADS) {
             if (f.nbuf == 8) return KNN_FUSED_FN(8, 8, 2);
+        }
+        if constexpr (KNN_FUSED_DEEP) {
+            if (f.nbuf == 6) return KNN_FUSED_FN(6, 8, 2);
         }
         return KNN_FUSED_FN(4, 8, 2);  // register lists always fit the pairs shape
     } else {
@@ -777,7 +870,8 @@ hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st) {
     const FilterPlan f = knn_fused_plan(a.d, a.k);
     if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != a.d + 16 || a.ld_q != a.d + 16 || !a.qstat)
         return hipErrorInvalidValue;
-    if (f.kr > 0 && !(f.nw == 8 && f.rg == 2 && (f.nbuf == 4 || (KNN_FUSED_QUADS && f.nbuf == 8))))
+    if (f.kr > 0 && !(f.nw == 8 && f.rg == 2 &&
+                      (f.nbuf == 4 || (KNN_FUSED_QUADS && f.nbuf == 8) || (KNN_FUSED_DEEP && f.nbuf == 6))))
         return hipErrorInvalidValue;  // (fused_fn_k)
     void* args[] = {const_cast<GemmFilterArgs*>(&a)};
     const dim3 grid((unsigned)(a.g2 < 0 ? (int64_t)a.n_qtiles * a.nseg : (int64_t)a.p1_blocks + a.g2));

@@ -69,3 +69,19 @@
 #else
 #define KNN_FUSED_QUADS 0
 #endif
+
+// KNN_STUDY_STAMPS: per-wave shader-clock stamps of the fused filter's loop (barrier wait, step,
+// slow path), summed over the launch into a device array (knn_debug_stamps).  Timing study only.
+#ifdef KNN_STUDY_STAMPS
+#define KNN_FUSED_STAMPS 1
+#else
+#define KNN_FUSED_STAMPS 0
+#endif
+
+// KNN_STUDY_DEEP: pairs with six buffers, the DMA two pairs ahead and counted vmcnt waits
+// (knn_fused_plan, register-list shapes with d <= 128).
+#ifdef KNN_STUDY_DEEP
+#define KNN_FUSED_DEEP 1
+#else
+#define KNN_FUSED_DEEP 0
+#endif

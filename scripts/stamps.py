@@ -16,13 +16,16 @@ lib = knn.load_library()
 lib.knn_debug_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 buf = (ctypes.c_ulonglong * 8)()
 dev = torch.device("cuda", 0)
-for name, nt, nq, d, k, seed in [("A", 1_000_000, 100_000, 128, 10, 1), ("B", 4_000_000, 1_000_000, 64, 32, 2)]:
+# (C1s: config C1's shard shape -- 4M bf16 rows x 256-d, k = 100 -- on 65,536 queries)
+for name, nt, nq, d, k, seed, bf in [("A", 1_000_000, 100_000, 128, 10, 1, 0), ("B", 4_000_000, 1_000_000, 64, 32, 2, 0),
+                                      ("C1s", 4_000_000, 65_536, 256, 100, 3, 1)]:
     ctx = knn.Context(0, algo="auto", profile=True)
-    train = torch.empty((nt, d), dtype=torch.float32, device=dev)
+    dt = torch.bfloat16 if bf else torch.float32
+    train = torch.empty((nt, d), dtype=dt, device=dev)
     labels = torch.empty(nt, dtype=torch.int32, device=dev)
-    test = torch.empty((nq, d), dtype=torch.float32, device=dev)
-    ctx.generate(train, labels, 0, d, 0, seed, 0, 10)
-    ctx.generate(test, None, 0, d, 0, seed, 1, 10)
+    test = torch.empty((nq, d), dtype=dt, device=dev)
+    ctx.generate(train, labels, 0, d, bf, seed, 0, 10)
+    ctx.generate(test, None, 0, d, bf, seed, 1, 10)
     pred = torch.empty(nq, dtype=torch.int32, device=dev)
     ctx.predict_device(train, labels, test, k, 10, pred)
     torch.cuda.synchronize()
