@@ -314,11 +314,14 @@ void certificate(int d, int felem, float* coef, float* eta) {
     }
 }
 
-// Fused-norm filter (knn_fused.hip): y = fl_mfma(sum -2 rq_i rt_i + tn_hi + tn_mid + tn_lo),
-// G = fl(qn + y), Delta = coef (qn + tn) + eta; rq, rt = the bf16 operands (q, t themselves
-// for bf16 data, rn(q), rn(t) for fp32 data).  With N = qn + tn (exact norms):
-//   MFMA accumulation of d + 3 terms at <= 2u per add, terms summing to <= 2.01 N: 4.02 (d+3) u N
-//   tn split hi + mid + lo (each subtraction exact): <= 2^-24 tn <= u N
+// Fused-norm filter (knn_fused.hip): y = fl_mfma(sum -2 rq_i rt_i + tn_hi + tn_mid + tn_lo)
+// (d = 64: the norm split over an augmented k-step), or y = fl_mfma(tn + sum -2 rq_i rt_i)
+// (d >= 128: the fp32 norm is the first MFMA's C operand), G = fl(qn + y), Delta = coef (qn +
+// tn) + eta; rq, rt = the bf16 operands (q, t themselves for bf16 data, rn(q), rn(t) for fp32
+// data).  With N = qn + tn (exact norms):
+//   MFMA accumulation of d + 3 terms (d + 1 with the C-operand norm) at <= 2u per add, terms
+//   summing to <= 2.01 N: 4.02 (d+3) u N
+//   tn split hi + mid + lo (each subtraction exact): <= 2^-24 tn <= u N (0 with the C operand)
 //   fp32 norms (fmaf chains): <= 1.01 d u each, 2.02 d u N;  G's rounding: <= 3.01 u N
 //   the reference's D vs the exact distance: <= 2 (d+2) u N
 // -> (8.04 d + 20.1) u N; the roundings of s, coef s, L and U and slack in 512 u N:
@@ -432,8 +435,25 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     const void* ftrain = tr->feat;
     const void* ftest = te->feat;
     int fld_t = tr->ld, fld_q = te->ld;
-    if (fused) {
-        // augmented bf16 rows: train [rn(t) | tn split], queries [-2 rn(q) | 1 1 1]
+    if (fused && knn_fused_row_bytes(d) == 2 * d) {
+        // d >= 128: train as tile blocks [bn rows of rn(t) | bn norms | tile statistics] (the
+        // filter starts each accumulator from the norms), queries as rn(-2 q) rows; one more
+        // tile of pad blocks past the grid (the filter scans tiles in twos, k_gemm_fused)
+        const int bn = 32 * knn_fused_plan(d, k).rg;
+        const int64_t ntf = ntp + 64;
+        const size_t tb = (size_t)bn * 2 * d + 4 * bn + 16;
+        HIP_OR_FAIL(c, c->split_t.ensure(tb * (size_t)(ntf / bn)));
+        HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * (size_t)d * nq));
+        stage_begin(c, st, gate ? "aug_rerun" : "aug");
+        HIP_OR_FAIL(c, knn_launch_tn_rows(tr->feat, dtype, ntf, nt, tr->ld, d, c->tnorm.as<float>(), 1.0f,
+                                          c->split_t.p, c->tmax.as<float4>(), bn, st, gate));
+        HIP_OR_FAIL(c, knn_launch_tn_rows(te->feat, dtype, nq, nq, te->ld, d, nullptr, -2.0f, c->split_q.p, nullptr,
+                                          0, st, gate));
+        stage_end(c, st);
+        ftrain = c->split_t.p; ftest = c->split_q.p;
+        fld_t = fld_q = d;
+    } else if (fused) {
+        // d = 64: augmented bf16 rows: train [rn(t) | tn split], queries [-2 rn(q) | 1 1 1]
         // (pad rows: zero features, a huge norm -- they never pass)
         // (one more tile of pad rows past the grid: the filter scans tiles in twos, k_gemm_fused)
         const int64_t ntf = ntp + 64;

@@ -200,6 +200,15 @@ __device__ __forceinline__ float o2f(uint32_t o) {
     return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
 
+// min / max of two non-NaN floats as one v_med3 (fminf/fmaxf add two canonicalising v_max in
+// IEEE mode): the middle of {a, b, -inf} is min(a, b), of {a, b, +inf} max(a, b)
+__device__ __forceinline__ float fmin_fast(float a, float b) {
+    return __builtin_amdgcn_fmed3f(a, b, __uint_as_float(0xff800000u));
+}
+__device__ __forceinline__ float fmax_fast(float a, float b) {
+    return __builtin_amdgcn_fmed3f(a, b, __uint_as_float(0x7f800000u));
+}
+
 __device__ __forceinline__ float f4get(const float4& v, int i) {
     return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
 }
@@ -282,15 +291,17 @@ __device__ __forceinline__ void wait_dma_barrier_n(int n) {
 __host__ __device__ __forceinline__ int heap_stride(int k) { return (k + 3 + 3) & ~3; }
 
 // tile geometry shared by the kernel and the host's LDS sizing: NW waves per block,
-// QG 32-query groups per wave, RG 32-row groups per tile; NACC = QG * RG accumulators
-template <int RB, int NW, int QG, int RG>
+// QG 32-query groups per wave, RG 32-row groups per tile; NACC = QG * RG accumulators;
+// HS header slots of 16 B after the rows (the fused filter's per-tile norms and statistics)
+template <int RB, int NW, int QG, int RG, int HS = 0>
 struct FilterTile {
     static constexpr int NACC = QG * RG;             // 32x32 accumulators per wave per tile
     static constexpr int BN = 32 * RG;               // train rows per tile
     static constexpr int BM = 32 * QG * NW;          // queries per block
     static constexpr int STRIDE = RB + 16;           // LDS bytes per tile row
     static constexpr int SLOTS = RB / 16 + 1;        // 16-B slots per padded row
-    static constexpr int DMA_INS = (BN * SLOTS + 63) / 64;     // 1 KiB DMA instructions per tile
-    static constexpr int LAST_LANES = BN * SLOTS - 64 * (DMA_INS - 1);  // active lanes of the last
-    static constexpr int TILE = DMA_INS * 1024;      // LDS bytes per buffer (>= BN * STRIDE)
+    static constexpr int DMA_INS = (BN * SLOTS + HS + 63) / 64;     // 1 KiB DMA instructions per tile
+    static constexpr int LAST_LANES = BN * SLOTS + HS - 64 * (DMA_INS - 1);  // active lanes of the last
+    static constexpr int TILE = DMA_INS * 1024;      // LDS bytes per buffer (>= BN * STRIDE + 16 HS)
+    static constexpr int HDR = BN * STRIDE;          // LDS offset of the header
 };

@@ -103,6 +103,76 @@ hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int64_t n_val
 }
 
 // ---------------------------------------------------------------------------------
+// k_tn_rows<E>: operand rows of the filter for d >= 128 (no augmented columns).
+//   queries (norms == NULL): [n][d] bf16 = rn(scale * x)
+//   train: blocks of bn rows, [bn][d] bf16 = rn(x) | bn fp32 norms | {max tn, max |t - rt|,
+//   max |rt|, 0} of the enclosing 64-row tile (k_row_norms) -- the image one tile's LDS-DMA
+//   copies, header included.  Rows n_valid .. n-1 (padding past the tile grid): zero features
+//   and norm 0x1.fep127, so y = tn - 2 q.t never passes a fast test.  n % bn == 0.
+// ---------------------------------------------------------------------------------
+template <typename E>
+__global__ __launch_bounds__(256) void k_tn_rows(const E* __restrict__ x, int64_t n, int64_t n_valid, int ld, int d,
+                                                 const float* __restrict__ norms, float scale,
+                                                 unsigned char* __restrict__ out, const float4* __restrict__ tstat,
+                                                 int bn, const int32_t* __restrict__ gate) {
+    if (gate && *gate == 0) return;
+    const int per_row = d >> 2;
+    auto quad = [&](int64_t r, int c) -> uint2 {
+        if (r >= n_valid) return make_uint2(0u, 0u);
+        const float4 v = load4(x + r * ld + c);
+        return make_uint2(bf16_rne(scale * v.x) | (bf16_rne(scale * v.y) << 16),
+                          bf16_rne(scale * v.z) | (bf16_rne(scale * v.w) << 16));
+    };
+    if (!norms) {
+        for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n * per_row; i += (int64_t)gridDim.x * 256) {
+            const int64_t r = i / per_row;
+            const int c = (int)(i - r * per_row) * 4;
+            *reinterpret_cast<uint2*>(out + (r * d + c) * 2) = quad(r, c);
+        }
+        return;
+    }
+    const int64_t per_tile = (int64_t)bn * per_row + bn + 1;
+    const int64_t tb = (int64_t)bn * d * 2 + 4 * bn + 16;
+    const int64_t nvt = (n_valid + 63) >> 6;  // 64-row tiles with statistics
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < (n / bn) * per_tile; i += (int64_t)gridDim.x * 256) {
+        const int64_t T = i / per_tile;
+        const int64_t l = i - T * per_tile;
+        const int64_t r0 = T * bn;
+        unsigned char* blk = out + T * tb;
+        if (l < (int64_t)bn * per_row) {
+            const int rr = (int)(l / per_row);
+            const int c = (int)(l - (int64_t)rr * per_row) * 4;
+            *reinterpret_cast<uint2*>(blk + ((int64_t)rr * d + c) * 2) = quad(r0 + rr, c);
+        } else if (l < (int64_t)bn * per_row + bn) {
+            const int rr = (int)(l - (int64_t)bn * per_row);
+            const int64_t r = r0 + rr;
+            *reinterpret_cast<float*>(blk + (int64_t)bn * d * 2 + 4 * rr) = r < n_valid ? norms[r] : 0x1.fep127f;
+        } else {
+            const int64_t t64 = r0 >> 6;
+            *reinterpret_cast<float4*>(blk + (int64_t)bn * d * 2 + 4 * bn) =
+                t64 < nvt ? tstat[t64] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
+    }
+}
+
+hipError_t knn_launch_tn_rows(const void* x, int elem, int64_t n, int64_t n_valid, int ld, int d, const float* norms,
+                              float scale, void* out, const float4* tstat, int bn, hipStream_t st,
+                              const int32_t* gate) {
+    if (n <= 0) return hipSuccess;
+    if (d % 4 || ld % 4 || (norms && (bn <= 0 || n % bn))) return hipErrorInvalidValue;
+    const int64_t total = norms ? (n / bn) * ((int64_t)bn * (d / 4) + bn + 1) : n * (d / 4);
+    const dim3 grid(elementwise_grid(total));
+    if (elem == ELEM_BF16)
+        hipLaunchKernelGGL(k_tn_rows<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, n, n_valid, ld, d, norms, scale,
+                           (unsigned char*)out, tstat, bn, gate);
+    else
+        hipLaunchKernelGGL(k_tn_rows<float>, grid, dim3(256), 0, st, (const float*)x, n, n_valid, ld, d, norms, scale,
+                           (unsigned char*)out, tstat, bn, gate);
+    KNN_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------------
 // k_gemm_fused<RB, MINW, NBUF, NW, RG>: the filter (RB = bytes per augmented row,
 // 2d + 32).  Block = NW waves x 32 queries; a train tile has BN = 32 RG rows, copied
 // global -> LDS by LDS-DMA (NBUF buffers, one barrier per tile, pieces issued between
@@ -141,12 +211,20 @@ extern "C" int knn_debug_stamps(unsigned long long* out, int reset) {
 template <int RB, int NBUF, int NW, int RG, int KR>
 __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int qt, const int seg,
                                             const int64_t row_begin, const int64_t row_end) {
-    typedef FilterTile<RB, NW, 1, RG> FT;
+    // TN (RB = 2d, d >= 128): train tiles carry their rows' norms in a header, and each
+    // accumulator starts from them (the MFMA's C operand) -- no augmented k-step.  Otherwise
+    // (RB = 2d + 32, d = 64) the norm rides in 16 augmented columns (one more k-step).
+    constexpr bool TN = RB % 64 == 0;
+    constexpr int BN_ = 32 * RG;
+    constexpr int HS = TN ? BN_ / 4 + 1 : 0;  // header slots: BN fp32 norms + the statistics
+    typedef FilterTile<RB, NW, 1, RG, HS> FT;
     constexpr int NACC = RG, BN = FT::BN, BM = FT::BM, STRIDE = FT::STRIDE, SLOTS = FT::SLOTS;
-    constexpr int DMA_INS = FT::DMA_INS, TILE = FT::TILE;
+    constexpr int DMA_INS = FT::DMA_INS, TILE = FT::TILE, HDR = FT::HDR;
+    // bytes of one tile in the train operand (TN: a block of rows + header; else rows of pitch RB)
+    constexpr int64_t TB = (int64_t)BN * RB + 16 * HS;
     constexpr int NT = 64 * NW;
     constexpr int DMA_PER_WAVE = (DMA_INS + NW - 1) / NW;
-    constexpr int NS = RB / 32;                  // k-steps: d/16 feature steps + the norm step
+    constexpr int NS = RB / 32;                  // k-steps: d/16 feature steps (+ the norm step)
     constexpr int VPS = (16 + NS - 1) / NS;      // fast-test values per k-step per accumulator
     static_assert(NBUF == 2 || NBUF == 4 || NBUF == 6 || NBUF == 8,
                   "tile buffers: two, four (tiles in pairs), six (pairs, DMA two pairs ahead) or eight (quads)");
@@ -222,11 +300,17 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // the tile's statistics, from row 0 of its LDS image (augmented columns d+8..d+10, see
     // k_aug_rows): one broadcast ds_read_b64, in order with the fragment reads -- no scalar
     // memory load in the loop
+    // (TN: the header's last slot, fp32)
     auto tile_q = [&](int buf) __attribute__((always_inline)) -> float2 {
-        const uint2 w = *reinterpret_cast<const uint2*>(tiles + buf * TILE + (RB - 16));
-        const float tx = __uint_as_float(w.x << 16), ty = __uint_as_float(w.x & 0xffff0000u);
-        const float tz = __uint_as_float(w.y << 16);
-        return make_float2(tx, fmaf(qe2, ty, eq2 * tz));
+        if constexpr (TN) {
+            const float4 w = *reinterpret_cast<const float4*>(tiles + buf * TILE + HDR + 4 * BN);
+            return make_float2(w.x, fmaf(qe2, w.y, eq2 * w.z));
+        } else {
+            const uint2 w = *reinterpret_cast<const uint2*>(tiles + buf * TILE + (RB - 16));
+            const float tx = __uint_as_float(w.x << 16), ty = __uint_as_float(w.x & 0xffff0000u);
+            const float tz = __uint_as_float(w.y << 16);
+            return make_float2(tx, fmaf(qe2, ty, eq2 * tz));
+        }
     };
 
     // tiles of the piece, rounded up to an even count: the scan loop below runs tiles in twos
@@ -245,13 +329,17 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
 #pragma unroll
     for (int i = 0; i < DMA_PER_WAVE; i++) {
         const int P = (wave + NW * i) * 64 + lane;
-        const int row = min(P / SLOTS, BN - 1), sl = P % SLOTS;
-        doff[i] = (uint32_t)(row * ldb + 16 * (sl == SLOTS - 1 ? 0 : sl));
+        if (TN && P >= BN * SLOTS) {  // header slot: norms, then the statistics
+            doff[i] = (uint32_t)(BN * RB + 16 * min(P - BN * SLOTS, HS - 1));
+        } else {
+            const int row = min(P / SLOTS, BN - 1), sl = P % SLOTS;
+            doff[i] = (uint32_t)(row * ldb + 16 * (sl == SLOTS - 1 ? 0 : sl));
+        }
     }
     const uint32_t lds_tiles = __builtin_amdgcn_readfirstlane(lds_addr(tiles));
     struct DmaTile { const unsigned char* src; uint32_t lds; };
     auto dma_desc = [&](int buf, int64_t r0) -> DmaTile {
-        return DmaTile{trainb + r0 * ldb, lds_tiles + (uint32_t)(buf * TILE)};
+        return DmaTile{trainb + (TN ? (r0 / BN) * TB : r0 * ldb), lds_tiles + (uint32_t)(buf * TILE)};
     };
     auto dma_piece = [&](int i, const DmaTile& d) __attribute__((always_inline)) {
         const int ins = wave + NW * i;
@@ -288,8 +376,25 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         const unsigned char* tile = tiles + buf * TILE;
         const unsigned char* a0p = tile + j * STRIDE + 16 * h;
         const unsigned char* a1p = tile + ((RG == 2 ? 32 : 0) + j) * STRIDE + 16 * h;
+        if constexpr (TN) {
+            // register r of accumulator c is row 32c + (r & 3) + 8 (r >> 2) + 4h: its norm starts
+            // the chain (four broadcast ds_read_b128 per accumulator)
+            const unsigned char* hn = tile + HDR + 4 * (4 * h);
 #pragma unroll
-        for (int c = 0; c < NACC; c++) X[c] = floatx16{};
+            for (int c = 0; c < NACC; c++) {
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const float4 v = *reinterpret_cast<const float4*>(hn + 4 * (32 * c + 8 * g));
+                    X[c][4 * g] = v.x;
+                    X[c][4 * g + 1] = v.y;
+                    X[c][4 * g + 2] = v.z;
+                    X[c][4 * g + 3] = v.w;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < NACC; c++) X[c] = floatx16{};
+        }
         float mn[NACC];
 #pragma unroll
         for (int c = 0; c < NACC; c++) mn[c] = INF;
@@ -472,7 +577,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     auto list_insert = [&](float w) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = LL - 1; i >= 1; i--) lst[i] = __builtin_amdgcn_fmed3f(lst[i - 1], w, lst[i]);
-        lst[0] = fminf(lst[0], w);
+        lst[0] = fmin_fast(lst[0], w);
     };
     // the other lane half's copy of a word (v_permlane32_swap: one of the swap's two results
     // is this lane's own word, the other its partner's)
@@ -539,7 +644,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                 if constexpr (HALVES) {
                     if (__ballot(w < INF)) {
                         list_insert(w);
-                        thr = fminf(thr, fmaxf(lst[LL - 1], partner(lst[LL - 1])));
+                        thr = fmin_fast(thr, __builtin_amdgcn_fmed3f(lst[LL - 1], partner(lst[LL - 1]), INF));
                     }
                 } else {
                     // (no lane inserting means no partner inserting: the swap waits for one)
@@ -547,7 +652,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                         const float wp = partner(w);  // the other half's candidate
                         list_insert(w);
                         list_insert(wp);
-                        thr = fminf(thr, lst[LL - 1]);
+                        thr = fmin_fast(thr, lst[LL - 1]);
                     }
                 }
             };
@@ -798,11 +903,17 @@ int knn_fused_schedule(GemmFilterArgs& a, int slots, int* nseg) {
 // ---------------------------------------------------------------------------------
 static size_t fused_lds_of(int row_bytes, int k, int nw, int rg, int nbuf, bool heaps) {
     const int bn = 32 * rg, bm = 32 * nw;
-    const int ins = (bn * (row_bytes / 16 + 1) + 63) / 64;
+    const int hs = row_bytes % 64 == 0 ? bn / 4 + 1 : 0;  // (k_gemm_fused: TN header slots)
+    const int ins = (bn * (row_bytes / 16 + 1) + hs + 63) / 64;
     return (size_t)nbuf * ins * 1024 + (heaps ? (size_t)bm * heap_stride(k) * sizeof(float) : 0);
 }
 
 bool knn_fused_supported(int d) { return d == 64 || d == 128 || d == 256; }
+
+// bytes per operand row in the tile image: d = 64 keeps the augmented block (2d + 32; its
+// LDS traffic per MFMA is the binding one there), d >= 128 starts the accumulators from the
+// norms in the tile header (2d)
+int knn_fused_row_bytes(int d) { return d == 64 ? 2 * d + 32 : 2 * d; }
 
 // Shapes (d = features; rows of 2d + 32 bytes).  Block = NW waves x 32 queries:
 //  * k <= 32 (register lists, KR = 16 / 32): 8 waves, 64-row tiles in pairs (four buffers,
@@ -815,7 +926,7 @@ bool knn_fused_supported(int d) { return d == 64 || d == 128 || d == 256; }
 // Register lists: k <= 16 keeps per-query lists (KR = 16), k <= 32 per-half lists (KR = 32,
 // 16 entries: exact 32-entry lists cost a block per CU of occupancy and 9 % of time on B).
 FilterPlan knn_fused_plan(int d, int k) {
-    const int rb = 2 * d + 32;
+    const int rb = knn_fused_row_bytes(d);
     const size_t cap = 160 * 1024 - 256;  // room for the kernel's static LDS
     const int kr = k <= 16 ? KNN_FUSED_SMALL_K_LIST : k <= 32 ? 32 : 0;
     auto make = [&](int nw, int rg, int minw, int nbuf) {
@@ -857,7 +968,7 @@ static const void* fused_fn(const FilterPlan& f) {
 }
 
 static const void* fused_ptr(int d, const FilterPlan& f) {
-    return d == 64 ? fused_fn<160>(f) : d == 128 ? fused_fn<288>(f) : fused_fn<544>(f);
+    return d == 64 ? fused_fn<160>(f) : d == 128 ? fused_fn<256>(f) : fused_fn<512>(f);
 }
 
 hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu) {
@@ -868,7 +979,8 @@ hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu) {
 
 hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st) {
     const FilterPlan f = knn_fused_plan(a.d, a.k);
-    if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != a.d + 16 || a.ld_q != a.d + 16 || !a.qstat)
+    const int ld = knn_fused_row_bytes(a.d) / 2;  // operand row pitch in elements
+    if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != ld || a.ld_q != ld || !a.qstat)
         return hipErrorInvalidValue;
     if (f.kr > 0 && !(f.nw == 8 && f.rg == 2 &&
                       (f.nbuf == 4 || (KNN_FUSED_QUADS && f.nbuf == 8) || (KNN_FUSED_DEEP && f.nbuf == 6))))
