@@ -12,18 +12,19 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 STEPS=${STEPS:-2}
 cd /tmp && export TMPDIR=/tmp
 OUT=$R/gpurun_out
+PT=${PROF_TAG:-prof}   # output dirs $OUT/${PT}_{trace,fetch,write,sq}
 BENCH="$R/bench.py --steps $STEPS --warmup 1 --no-cpu-baseline --no-host-path ${BENCH_ARGS:-}"
 
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_trace -o run \
-    -- python3 $BENCH > $OUT/prof_trace.log 2>&1 || { echo "trace pass failed"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${PT}_trace -o run \
+    -- python3 $BENCH > $OUT/${PT}_trace.log 2>&1 || { echo "trace pass failed"; exit 1; }
 echo "trace pass ok"
-timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof_fetch -o run \
-    -- python3 $BENCH > $OUT/prof_fetch.log 2>&1 || { echo "fetch pass failed"; exit 1; }
+timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/${PT}_fetch -o run \
+    -- python3 $BENCH > $OUT/${PT}_fetch.log 2>&1 || { echo "fetch pass failed"; exit 1; }
 echo "fetch pass ok"
-timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof_write -o run \
-    -- python3 $BENCH > $OUT/prof_write.log 2>&1 || { echo "write pass failed"; exit 1; }
+timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/${PT}_write -o run \
+    -- python3 $BENCH > $OUT/${PT}_write.log 2>&1 || { echo "write pass failed"; exit 1; }
 echo "write pass ok"
 timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
-    --output-format csv -d $OUT/prof_sq -o run \
-    -- python3 $BENCH > $OUT/prof_sq.log 2>&1 || { echo "sq pass failed"; exit 1; }
+    --output-format csv -d $OUT/${PT}_sq -o run \
+    -- python3 $BENCH > $OUT/${PT}_sq.log 2>&1 || { echo "sq pass failed"; exit 1; }
 echo "sq pass ok"

@@ -1,6 +1,6 @@
 """Summarise the rocprofv3 outputs of scripts/profile_bench.sh into profiles/.
 
-    python scripts/summarize_profile.py TAG [gpurun_out] [CONFIG]
+    python scripts/summarize_profile.py TAG [gpurun_out] [CONFIG] [PROF_TAG]
 
 Writes profiles/TAG_kernel_stats.csv (the --stats summary as produced),
 profiles/TAG_pmc_traffic.json (per-launch HBM bytes of k_gemm_filter with the gfx950
@@ -22,18 +22,19 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     tag = sys.argv[1]
     src = sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "gpurun_out")
+    pt = sys.argv[4] if len(sys.argv) > 4 else "prof"  # profile_bench.sh PROF_TAG
     prof = os.path.join(REPO, "profiles")
     os.makedirs(prof, exist_ok=True)
-    shutil.copy(os.path.join(src, "prof_trace", "run_kernel_stats.csv"),
+    shutil.copy(os.path.join(src, pt + "_trace", "run_kernel_stats.csv"),
                 os.path.join(prof, f"{tag}_kernel_stats.csv"))
     # durations per kernel from the trace
     dur = defaultdict(list)
-    with open(os.path.join(src, "prof_trace", "run_kernel_trace.csv")) as f:
+    with open(os.path.join(src, pt + "_trace", "run_kernel_trace.csv")) as f:
         for r in csv.DictReader(f):
             dur[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
     counters = defaultdict(lambda: defaultdict(list))
     rows_out = []
-    for p in ("prof_fetch", "prof_write", "prof_sq"):
+    for p in (pt + "_fetch", pt + "_write", pt + "_sq"):
         path = os.path.join(src, p, "run_counter_collection.csv")
         if not os.path.exists(path):
             continue
