@@ -436,7 +436,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     const void* ftest = te->feat;
     int fld_t = tr->ld, fld_q = te->ld;
     if (fused && knn_fused_row_bytes(d) == 2 * d) {
-        // d >= 128: train as tile blocks [bn rows of rn(t) | bn norms | tile statistics] (the
+        // train as tile blocks [bn rows of rn(t) | bn norms | tile statistics] (the
         // filter starts each accumulator from the norms), queries as rn(-2 q) rows; one more
         // tile of pad blocks past the grid (the filter scans tiles in twos, k_gemm_fused)
         const int bn = 32 * knn_fused_plan(d, k).rg;
@@ -453,7 +453,8 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         ftrain = c->split_t.p; ftest = c->split_q.p;
         fld_t = fld_q = d;
     } else if (fused) {
-        // d = 64: augmented bf16 rows: train [rn(t) | tn split], queries [-2 rn(q) | 1 1 1]
+        // (study build KNN_STUDY_AUG64, d = 64) augmented bf16 rows: train [rn(t) | tn split],
+        // queries [-2 rn(q) | 1 1 1]
         // (pad rows: zero features, a huge norm -- they never pass)
         // (one more tile of pad rows past the grid: the filter scans tiles in twos, k_gemm_fused)
         const int64_t ntf = ntp + 64;

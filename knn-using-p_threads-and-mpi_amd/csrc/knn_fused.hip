@@ -103,7 +103,7 @@ hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int64_t n_val
 }
 
 // ---------------------------------------------------------------------------------
-// k_tn_rows<E>: operand rows of the filter for d >= 128 (no augmented columns).
+// k_tn_rows<E>: operand rows of the filter (no augmented columns).
 //   queries (norms == NULL): [n][d] bf16 = rn(scale * x)
 //   train: blocks of bn rows, [bn][d] bf16 = rn(x) | bn fp32 norms | {max tn, max |t - rt|,
 //   max |rt|, 0} of the enclosing 64-row tile (k_row_norms) -- the image one tile's LDS-DMA
@@ -211,9 +211,10 @@ extern "C" int knn_debug_stamps(unsigned long long* out, int reset) {
 template <int RB, int NBUF, int NW, int RG, int KR>
 __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int qt, const int seg,
                                             const int64_t row_begin, const int64_t row_end) {
-    // TN (RB = 2d, d >= 128): train tiles carry their rows' norms in a header, and each
+    // TN (RB = 2d, the product): train tiles carry their rows' norms in a header, and each
     // accumulator starts from them (the MFMA's C operand) -- no augmented k-step.  Otherwise
-    // (RB = 2d + 32, d = 64) the norm rides in 16 augmented columns (one more k-step).
+    // (RB = 2d + 32, the KNN_STUDY_AUG64 build at d = 64) the norm rides in 16 augmented columns
+    // (one more k-step).
     constexpr bool TN = RB % 64 == 0;
     constexpr int BN_ = 32 * RG;
     constexpr int HS = TN ? BN_ / 4 + 1 : 0;  // header slots: BN fp32 norms + the statistics
@@ -325,6 +326,8 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // rows) and rejected by index).  Every tile is whole: the augmented train rows are padded to
     // the 64-row grid (run_gemm), so a piece is always the scalar tile base + this lane's fixed
     // offset -- no per-tile address arithmetic in VGPRs.
+    // (piece ins = wave + NW i; rotating the DMA_INS % NW remainder pieces between even and odd
+    // tiles, so no wave issues two more per pair than another, measured no faster: r03r)
     uint32_t doff[DMA_PER_WAVE];
 #pragma unroll
     for (int i = 0; i < DMA_PER_WAVE; i++) {
@@ -344,7 +347,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     auto dma_piece = [&](int i, const DmaTile& d) __attribute__((always_inline)) {
         const int ins = wave + NW * i;
         if (ins < DMA_INS) {
-            if (i == DMA_PER_WAVE - 1 && ins == DMA_INS - 1 && lane >= FT::LAST_LANES) return;
+            if (ins == DMA_INS - 1 && lane >= FT::LAST_LANES) return;
             dma16s(doff[i], d.src, d.lds + (uint32_t)ins * 1024u);
         }
     };
@@ -599,6 +602,8 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         for (int c = 0; c < NACC; c++) {
             if (!((u >> (16 * c)) & 1u)) continue;  // (wave-uniform) no lane passes in c
             // round 1: the highest passing index, its value, the lane's passing count
+            // (a scan of the 16 values; scanning the highest passing group of four instead,
+            // found by the group minima, measured 4-8 % slower overall: r03q)
             int idx = -1, cnt = 0;
             float yv = INF;
 #pragma unroll
@@ -687,24 +692,34 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         qcnt = 0;
         publish();
     };
+    // (the heap shapes visit the passing positions wave-wide: per value only a queue append,
+    // so the lane-parallel scan would cost more than it saves -- C1 259.8 vs 273.3 ms, r03p)
     auto record = [&](floatx16 (&Y)[NACC], int tp, float tf, float2 tq, uint32_t u) {
         const int64_t tbase = row_begin + (int64_t)tp * BN;
-        lane_rounds(Y, tf, u, [&](int c, int idx, float yv) __attribute__((always_inline)) {
-            if (__ballot(idx >= 0 && qcnt >= RQ)) flush();
-            const int row = 32 * c + (idx & 3) + 8 * (idx >> 2) + 4 * h;
+        u = pass_set(Y, tf, u);
+        while (u) {
+            const int v = __builtin_ctz(u);
+            u &= u - 1u;
+            const float y = yval(Y, v);
+            const bool p = y <= tf;
+            if (__ballot(p && qcnt >= RQ)) flush();
+            const int r = v & 15;
+            const int row = 32 * (v >> 4) + (r & 3) + 8 * (r >> 2) + 4 * h;
             const int64_t t = tbase + row;
-            float L, U;
-            bounds(yv, tq, L, U);
-            if (idx >= 0 && t < row_end && L <= thr) {
+            if (p && t < row_end) {
+                float L, U;
+                bounds(y, tq, L, U);
+                if (L <= thr) {
 #pragma unroll
-                for (int i = 0; i < RQ; i++) {
-                    qL[i] = i == qcnt ? L : qL[i];
-                    qU[i] = i == qcnt ? U : qU[i];
-                    qT[i] = i == qcnt ? (int)t : qT[i];
+                    for (int i = 0; i < RQ; i++) {
+                        qL[i] = i == qcnt ? L : qL[i];
+                        qU[i] = i == qcnt ? U : qU[i];
+                        qT[i] = i == qcnt ? (int)t : qT[i];
+                    }
+                    qcnt++;
                 }
-                qcnt++;
             }
-        });
+        }
     };
 
     floatx16 accA[NACC], accB[NACC];
@@ -751,7 +766,10 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             if (it % GRP == 0)
                 wait_dma_barrier_n(npw * ((it + 2 < ntiles ? 1 : 0) + (it + 3 < ntiles ? 1 : 0)));
         } else {
-            if (!PAIR || it % GRP == 0) wait_dma_barrier();
+            if (!PAIR || it % GRP == 0) {
+                if constexpr (KNN_STUDY_NO_BARRIER) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                else wait_dma_barrier();
+            }
         }
         const uint64_t t1 = now();
         // this tile's terms, for its fast test in the next iteration (the tile is resident:
@@ -910,10 +928,10 @@ static size_t fused_lds_of(int row_bytes, int k, int nw, int rg, int nbuf, bool 
 
 bool knn_fused_supported(int d) { return d == 64 || d == 128 || d == 256; }
 
-// bytes per operand row in the tile image: d = 64 keeps the augmented block (2d + 32; its
-// LDS traffic per MFMA is the binding one there), d >= 128 starts the accumulators from the
-// norms in the tile header (2d)
-int knn_fused_row_bytes(int d) { return d == 64 ? 2 * d + 32 : 2 * d; }
+// bytes per operand row in the tile image: 2d -- the accumulators start from the norms in the
+// tile header (B, d = 64: 614 -> 586 ms against the augmented k-step, r03q); the augmented block
+// (2d + 32) stays as the study build KNN_STUDY_AUG64
+int knn_fused_row_bytes(int d) { return d == 64 && KNN_FUSED_AUG64 ? 2 * d + 32 : 2 * d; }
 
 // Shapes (d = features; rows of 2d + 32 bytes).  Block = NW waves x 32 queries:
 //  * k <= 32 (register lists, KR = 16 / 32): 8 waves, 64-row tiles in pairs (four buffers,
@@ -968,7 +986,8 @@ static const void* fused_fn(const FilterPlan& f) {
 }
 
 static const void* fused_ptr(int d, const FilterPlan& f) {
-    return d == 64 ? fused_fn<160>(f) : d == 128 ? fused_fn<256>(f) : fused_fn<512>(f);
+    if (d == 64) return KNN_FUSED_AUG64 ? fused_fn<160>(f) : fused_fn<128>(f);
+    return d == 128 ? fused_fn<256>(f) : fused_fn<512>(f);
 }
 
 hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu) {

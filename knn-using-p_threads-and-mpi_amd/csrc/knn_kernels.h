@@ -163,7 +163,7 @@ hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st);
 hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int64_t n_valid, int ld, int d, const float* norms,
                                float scale, uint16_t* out, const float4* tstat, hipStream_t st,
                                const int32_t* gate = nullptr);
-// d >= 128 (knn_fused_row_bytes(d) == 2d): x -> queries [n][d] bf16 rn(scale x) (norms == NULL),
+// knn_fused_row_bytes(d) == 2d: x -> queries [n][d] bf16 rn(scale x) (norms == NULL),
 // or train blocks of bn rows [bn][d] bf16 | bn fp32 norms | tstat of the enclosing 64-row tile
 hipError_t knn_launch_tn_rows(const void* x, int elem, int64_t n, int64_t n_valid, int ld, int d, const float* norms,
                               float scale, void* out, const float4* tstat, int bn, hipStream_t st,

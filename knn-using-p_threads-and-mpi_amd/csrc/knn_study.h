@@ -23,7 +23,16 @@
 #define KNN_STUDY_NO_DMA 0
 #endif
 
-#if KNN_STUDY_NO_SLOW || KNN_STUDY_NO_EPI || KNN_STUDY_NO_DMA
+// KNN_ABLATE_NO_BARRIER: the fused filter's tile barrier keeps its waits but drops the s_barrier
+// (results invalid: waves may read tiles other waves' DMAs have not landed) -- prices the
+// cross-wave synchronisation.
+#ifdef KNN_ABLATE_NO_BARRIER
+#define KNN_STUDY_NO_BARRIER 1
+#else
+#define KNN_STUDY_NO_BARRIER 0
+#endif
+
+#if KNN_STUDY_NO_SLOW || KNN_STUDY_NO_EPI || KNN_STUDY_NO_DMA || KNN_STUDY_NO_BARRIER
 // the fallback scan is skipped (results invalid) ...
 #define KNN_STUDY_SKIP_FALLBACK(qlist) \
     do {                               \
@@ -85,3 +94,12 @@
 #else
 #define KNN_FUSED_DEEP 0
 #endif
+
+// KNN_STUDY_AUG64: d = 64 keeps the norm in an augmented k-step (2d + 32 bytes per row) instead
+// of starting its accumulators from the tile header's norms (knn_fused_row_bytes).
+#ifdef KNN_STUDY_AUG64
+#define KNN_FUSED_AUG64 1
+#else
+#define KNN_FUSED_AUG64 0
+#endif
+
