@@ -63,6 +63,7 @@ struct knn_ctx {
     DBuf pad_t;             // KNN_ALGO_GEMM, n_train not a multiple of 64: the rows padded to the tile grid
     DBuf seg_rec;           // k_direct_tile segment records [nseg][nq][3][k]
     DBuf tmax;              // fused filter: per-64-row train stats {max tn, max |t - rt|, max |rt|, 0}
+    DBuf cursor;            // fused filter: per-XCD scan cursors (64-row units; performance hint only)
     DBuf qstat;             // fused filter: per-query {|q|, |q - rq|} upper bounds
     int rescore_su = 0;  // test hook KNN_RESCORE_SU: the rescore's LDS staging size (0 = sized)
     // host-API staging (device copies of host inputs / outputs)
@@ -527,6 +528,15 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     g.gthr = c->gthr.as<uint32_t>();
     g.cnt = c->cnt.as<int32_t>(); g.cand = c->cand.as<CandRec>(); g.cap = cap; g.cap_seg = cap / nseg;
     g.qstat = fused ? c->qstat.as<float2>() : nullptr;
+    // per-XCD scan cursors for the multi-segment schedule (B: filter traffic beyond L2 664 ->
+    // 494 GB per launch, time unchanged; with one segment or the balanced schedule they saved
+    // nothing: r03s).  KNN_NO_SCAN_CURSOR=1 turns them off (a diagnostic; same results).
+    static const bool no_cursor = getenv("KNN_NO_SCAN_CURSOR") != nullptr;
+    if (fused && !no_cursor && g.g2 < 0 && nseg > 1) {
+        HIP_OR_FAIL(c, c->cursor.ensure(sizeof(uint32_t) * 8));
+        HIP_OR_FAIL(c, hipMemsetAsync(c->cursor.p, 0, sizeof(uint32_t) * 8, st));
+        g.cursor = c->cursor.as<uint32_t>();
+    }
     g.status = c->ctrl.as<int32_t>();
     g.gate = gate;
     if (fused && g.g2 >= 0 && nseg > 1)  // whole query tiles write only sub-slice 0
@@ -631,7 +641,7 @@ void knn_destroy(knn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (DBuf* b : {&c->tnorm, &c->tnp, &c->qnorm, &c->gthr, &c->cnt, &c->cand,
-                    &c->fb_list, &c->ctrl, &c->scratch, &c->split_t, &c->split_q, &c->pad_t, &c->seg_rec, &c->tmax, &c->qstat, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
+                    &c->fb_list, &c->ctrl, &c->scratch, &c->split_t, &c->split_q, &c->pad_t, &c->seg_rec, &c->tmax, &c->qstat, &c->cursor, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
                     &c->h_dist, &c->h_idx})
         b->release();
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);

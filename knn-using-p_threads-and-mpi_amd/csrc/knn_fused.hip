@@ -320,6 +320,33 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // next 64 rows (another piece's, or the padding the augmented train rows carry past the
     // tile grid, run_gemm), which the row_end test rejects.
     const int ntiles = (row_end > row_begin) ? ((int)((row_end - row_begin + BN - 1) / BN) + 1) & ~1 : 0;
+    // Scan order (a.cursor set: the host does so for the multi-segment schedule): the piece's
+    // tiles rotated to start where this XCD's other blocks are (per XCD: the 64-row unit the last
+    // block to publish was at, if inside this piece) -- so the blocks one XCD runs at once
+    // stream the same rows through its L2 instead of drifting apart (blocks are dispatched to
+    // the XCDs round-robin).  Correctness does not depend on the order: every tile is scanned
+    // once and the threshold logic is order-free.
+    // All waves of the block must use the same order (they DMA pieces of the same tiles): thread
+    // 0 reads the cursor and hands the rotation to the others through LDS (blk_rot, written
+    // before the block barrier below, read after it).
+    const int xcd = blockIdx.x & 7;
+    int* blk_rot = reinterpret_cast<int*>(smem + NBUF * TILE + (RL ? 0 : BM * hs * (int)sizeof(float)));
+    if (threadIdx.x == 0) {
+        int r0 = 0;
+        if (a.cursor && ntiles > 0) {
+            const int64_t cu =
+                (int64_t)__hip_atomic_load(&a.cursor[xcd], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * 64;
+            if (cu > row_begin && cu < row_end) r0 = (int)((cu - row_begin) / BN);
+        }
+        *blk_rot = r0;
+    }
+    int rot = 0;  // (set after the barrier)
+    // the first row of logical tile t (t < ntiles): physical tile (t + rot) mod ntiles
+    auto tile_row = [&](int t) __attribute__((always_inline)) -> int64_t {
+        int pt = t + rot;
+        pt = pt >= ntiles ? pt - ntiles : pt;
+        return row_begin + (int64_t)pt * BN;
+    };
 
     // ---- LDS-DMA of tiles (same image as k_gemm_filter: slot P -> row P / SLOTS, slot P % SLOTS,
     // the pad slot duplicates slot 0; rows past row_end are read (padding or the next piece's
@@ -535,7 +562,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // immediate slow path (4-wave heap shapes): the passing values of tile tp, visited by
     // index; the two lanes of a query take turns (one heap writer at a time)
     auto slow = [&](floatx16 (&Y)[NACC], int tp, float tf, float2 tq, uint32_t u) {
-        const int64_t tbase = row_begin + (int64_t)tp * BN;
+        const int64_t tbase = tile_row(tp);
         u = pass_set(Y, tf, u);
         while (u) {
             const int v = __builtin_ctz(u);
@@ -604,6 +631,8 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             // round 1: the highest passing index, its value, the lane's passing count
             // (a scan of the 16 values; scanning the highest passing group of four instead,
             // found by the group minima, measured 4-8 % slower overall: r03q)
+            // (detecting "some lane passes twice" from the compares' wave masks with scalar ops
+            // instead of the count measured 2.7 % slower on B: r03s)
             int idx = -1, cnt = 0;
             float yv = INF;
 #pragma unroll
@@ -637,7 +666,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     };
     auto slow_rl = [&](floatx16 (&Y)[NACC], int tp, float tf, float2 tq, uint32_t u) {
         if constexpr (RL) {
-            const int64_t tbase = row_begin + (int64_t)tp * BN;
+            const int64_t tbase = tile_row(tp);
             auto visit = [&](int c, int idx, float yv) __attribute__((always_inline)) {
                 const int row = 32 * c + (idx & 3) + 8 * (idx >> 2) + 4 * h;
                 const int64_t t = tbase + row;
@@ -695,7 +724,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // (the heap shapes visit the passing positions wave-wide: per value only a queue append,
     // so the lane-parallel scan would cost more than it saves -- C1 259.8 vs 273.3 ms, r03p)
     auto record = [&](floatx16 (&Y)[NACC], int tp, float tf, float2 tq, uint32_t u) {
-        const int64_t tbase = row_begin + (int64_t)tp * BN;
+        const int64_t tbase = tile_row(tp);
         u = pass_set(Y, tf, u);
         while (u) {
             const int v = __builtin_ctz(u);
@@ -725,11 +754,12 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     floatx16 accA[NACC], accB[NACC];
 #pragma unroll
     for (int c = 0; c < NACC; c++) accA[c] = accB[c] = floatx16{};
-    __syncthreads();  // LDS init is complete before any DMA lands
+    __syncthreads();  // LDS init is complete before any DMA lands; blk_rot is written
+    rot = __builtin_amdgcn_readfirstlane(*blk_rot);
 #pragma unroll
     for (int p = 0; p < AHEAD; p++)
         if (p < ntiles) {
-            const DmaTile d0 = dma_desc(p, row_begin + (int64_t)p * BN);
+            const DmaTile d0 = dma_desc(p, tile_row(p));
 #pragma unroll
             for (int i = 0; i < DMA_PER_WAVE; i++) dma_piece(i, d0);
         }
@@ -737,13 +767,16 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // tile terms (max norm, rounding bound) of the tile in the pipeline (it) and of tile it-1
     float2 tm_prev = make_float2(0.0f, 0.0f);
     // study build KNN_STUDY_STAMPS: shader-clock stamps per wave (barrier wait, step, slow path)
-    uint64_t st_bar = 0, st_step = 0, st_slow = 0, st_visits = 0;
-    const uint64_t st_start = KNN_FUSED_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    [[maybe_unused]] uint64_t st_bar = 0, st_step = 0, st_slow = 0, st_visits = 0;
+    [[maybe_unused]] const uint64_t st_start = KNN_FUSED_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     auto now = [&]() __attribute__((always_inline)) -> uint64_t {
         return KNN_FUSED_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     };
     auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
         if ((it & (FUSED_SHARE_EVERY - 1)) == FUSED_SHARE_EVERY - 1) {
+            if (a.cursor && threadIdx.x == 0)
+                __hip_atomic_store(&a.cursor[xcd], (uint32_t)(tile_row(it) >> 6), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             if (a.nseg > 1 && qvalid) {
                 if constexpr (RL) {  // publish this query's bound (the heap path does it per accept)
                     if (h == 0 && thr < published) {
@@ -776,7 +809,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         // landed before this step's barrier, not overwritten before the next one)
         const float2 tm_cur = tile_q(it % NBUF);
         const bool dma_on = !KNN_STUDY_NO_DMA && it + AHEAD < ntiles;
-        const DmaTile dd = dma_desc((it + AHEAD) % NBUF, row_begin + (int64_t)(it + AHEAD) * BN);
+        const DmaTile dd = dma_desc((it + AHEAD) % NBUF, tile_row(it + AHEAD));
         const float tf = it > 0 ? tf_of(tm_prev) : -INF;
         const uint32_t uY = step(X, Y, it % NBUF, dma_on, dd, tf, PAIR && it % GRP != 0);
         // PAIR: the pair's next tile is resident since its barrier -- its first fragments are
@@ -923,7 +956,8 @@ static size_t fused_lds_of(int row_bytes, int k, int nw, int rg, int nbuf, bool 
     const int bn = 32 * rg, bm = 32 * nw;
     const int hs = row_bytes % 64 == 0 ? bn / 4 + 1 : 0;  // (k_gemm_fused: TN header slots)
     const int ins = (bn * (row_bytes / 16 + 1) + hs + 63) / 64;
-    return (size_t)nbuf * ins * 1024 + (heaps ? (size_t)bm * heap_stride(k) * sizeof(float) : 0);
+    // (+ 16 bytes: the block's scan rotation, k_gemm_fused)
+    return (size_t)nbuf * ins * 1024 + (heaps ? (size_t)bm * heap_stride(k) * sizeof(float) : 0) + 16;
 }
 
 bool knn_fused_supported(int d) { return d == 64 || d == 128 || d == 256; }

@@ -56,6 +56,7 @@ struct GemmFilterArgs {
     // fused filter schedule (knn_fused_schedule): p1_blocks whole query tiles, then g2 blocks
     // over the remaining w2 (query tile, 64-row unit) pairs; tiles64 units per query tile
     int p1_blocks; int g2; int64_t w2; int64_t tiles64;
+    uint32_t* cursor;       // fused filter, optional: per XCD, the 64-row unit its blocks scan now
     const int32_t* status;  // the call's status word: a set GEMM_UNSAFE bit skips the filter
     const int32_t* gate;    // optional: the filter runs only when *gate != 0 (AUTO's re-run)
 };
