@@ -383,7 +383,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     auto dma_at = [&](int s, bool on, const DmaTile& d) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < DMA_PER_WAVE; i++)
-            if (on && (i * NS) / DMA_PER_WAVE == s) dma_piece(i, d);
+            if (on && (KNN_FUSED_EARLY_DMA ? i : (i * NS) / DMA_PER_WAVE) == s) dma_piece(i, d);
     };
 
     // ---- one tile's MFMAs into X; in between, the fast test of the previous tile (Y): a v_min3

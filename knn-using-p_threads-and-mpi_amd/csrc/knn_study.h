@@ -103,3 +103,11 @@
 #define KNN_FUSED_AUG64 0
 #endif
 
+
+// KNN_STUDY_EARLY_DMA: the step's DMA pieces in its first k-steps (piece i in k-step i) instead
+// of spread over the step.
+#ifdef KNN_STUDY_EARLY_DMA
+#define KNN_FUSED_EARLY_DMA 1
+#else
+#define KNN_FUSED_EARLY_DMA 0
+#endif
