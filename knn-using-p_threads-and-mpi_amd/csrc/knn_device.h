@@ -272,19 +272,6 @@ __device__ __forceinline__ void dma4s(uint32_t voff, const void* sbase, uint32_t
 __device__ __forceinline__ void wait_dma_barrier() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
-// the same with up to n (wave-uniform, <= 15) of this wave's youngest vector-memory ops left in
-// flight: they retire in issue order, so everything older -- the DMAs of the tiles about to be
-// read, when the n youngest are the next tiles' DMAs (or later stores) -- has landed
-__device__ __forceinline__ void wait_dma_barrier_n(int n) {
-#define KNN_WAIT_CASE(N) case N: asm volatile("s_waitcnt vmcnt(" #N ") lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
-    switch (n) {
-        KNN_WAIT_CASE(1) KNN_WAIT_CASE(2) KNN_WAIT_CASE(3) KNN_WAIT_CASE(4) KNN_WAIT_CASE(5)
-        KNN_WAIT_CASE(6) KNN_WAIT_CASE(7) KNN_WAIT_CASE(8) KNN_WAIT_CASE(9) KNN_WAIT_CASE(10)
-        KNN_WAIT_CASE(11) KNN_WAIT_CASE(12) KNN_WAIT_CASE(13) KNN_WAIT_CASE(14) KNN_WAIT_CASE(15)
-        default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
-    }
-#undef KNN_WAIT_CASE
-}
 
 // per-query 4-ary heap stride in floats: node n >= 1 in slot n-1, the root in the last slot;
 // slots of nodes >= k hold -inf up to the last child group a parent < k reads (slot k+1)

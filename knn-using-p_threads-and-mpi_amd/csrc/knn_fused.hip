@@ -227,23 +227,19 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     constexpr int DMA_PER_WAVE = (DMA_INS + NW - 1) / NW;
     constexpr int NS = RB / 32;                  // k-steps: d/16 feature steps (+ the norm step)
     constexpr int VPS = (16 + NS - 1) / NS;      // fast-test values per k-step per accumulator
-    static_assert(NBUF == 2 || NBUF == 4 || NBUF == 6 || NBUF == 8,
-                  "tile buffers: two, four (tiles in pairs), six (pairs, DMA two pairs ahead) or eight (quads)");
+    static_assert(NBUF == 2 || NBUF == 4, "tile buffers: two, or four (tiles in pairs)");
     // NBUF = 4: tiles go in pairs -- one barrier per pair; the DMA of tile it + 2 is issued
     // during step it into the buffer tile it - 2 used (read before this pair's barrier)
-    // (NBUF = 8: groups of four tiles, one barrier per four, DMA four tiles ahead; NBUF = 6:
-    // pairs with the DMA two pairs ahead -- a pair's barrier waits only for its own tiles'
-    // pieces, the next pair's stay in flight: vmcnt(pieces issued since))
-    constexpr int GRP = NBUF == 8 ? 4 : NBUF >= 4 ? 2 : 1;
+    // (quads -- eight buffers, one barrier per four tiles -- and six-buffer pairs with the DMA
+    // two pairs ahead and counted vmcnt waits measured no faster: DESIGN.md, round-3 studies)
+    constexpr int GRP = NBUF == 4 ? 2 : 1;
     constexpr bool PAIR = GRP > 1;
-    constexpr bool DEEP = NBUF == 6;
-    constexpr int AHEAD = DEEP ? 4 : PAIR ? GRP : NBUF - 1;  // tiles between a step and the tile it DMAs
+    constexpr int AHEAD = PAIR ? GRP : NBUF - 1;  // tiles between a step and the tile it DMAs
     static_assert(RG == 1 || RG == 2, "row groups");
-    static_assert(KR == 0 || KR == 8 || KR == 16 || KR == 32,
-                  "register lists: k <= 16 (shared 16 or per-half 8 entries), k <= 32, or LDS heaps");
+    static_assert(KR == 0 || KR == 16 || KR == 32, "register lists: k <= 16, k <= 32, or LDS heaps");
     constexpr bool RL = KR > 0;                   // thresholds from per-lane register lists (else LDS heaps)
-    constexpr bool HALVES = KR == 32 || KR == 8;  // one list per lane half (below): k <= 2 LL
-    constexpr int LL = KR == 8 ? 8 : 16;          // register list length
+    constexpr bool HALVES = KR == 32;             // one list per lane half (below): k <= 2 LL
+    constexpr int LL = 16;                        // register list length
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* tiles = smem;                                     // [NBUF][TILE]
     const int hs = heap_stride(a.k);
@@ -378,12 +374,11 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             dma16s(doff[i], d.src, d.lds + (uint32_t)ins * 1024u);
         }
     };
-    const int npw = (DMA_INS - wave + NW - 1) / NW;  // DMA instructions this wave issues per tile
     // piece i goes out in k-step (i NS) / DMA_PER_WAVE of the step
     auto dma_at = [&](int s, bool on, const DmaTile& d) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < DMA_PER_WAVE; i++)
-            if (on && (KNN_FUSED_EARLY_DMA ? i : (i * NS) / DMA_PER_WAVE) == s) dma_piece(i, d);
+            if (on && (i * NS) / DMA_PER_WAVE == s) dma_piece(i, d);
     };
 
     // ---- one tile's MFMAs into X; in between, the fast test of the previous tile (Y): a v_min3
@@ -593,7 +588,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // their candidate U (v_permlane32_swap) and both insert both (32 v_med3, the multiset and
     // so the list come out the same in either order): the query's exact k-th smallest, like
     // the heap, for all 32 queries of the wave at once -- no LDS, no lane takes turns.
-    // HALVES (16 < k <= 32, KR = 32; KR = 8: k <= 16 with 8-entry lists): each lane keeps its own
+    // HALVES (16 < k <= 32, KR = 32): each lane keeps its own
     // half's ceil(k/2) smallest U (LL - ceil(k/2) pads) and inserts only its own values (LL
     // v_med3); the bound is the larger of the two
     // halves' ceil(k/2)-th smallest -- at least 2 ceil(k/2) >= k kept rows have U <= it.  A
@@ -793,16 +788,9 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         // waits for all of its own vector-memory ops, then the barrier -- and every wave is done
         // with the buffers the next DMAs overwrite
         const uint64_t t0 = now();
-        if constexpr (DEEP) {
-            // this wave's pieces of tiles it + 2, it + 3 (DMA'd during the previous pair, or by
-            // the prologue) may stay in flight; everything older -- this pair's tiles -- lands
-            if (it % GRP == 0)
-                wait_dma_barrier_n(npw * ((it + 2 < ntiles ? 1 : 0) + (it + 3 < ntiles ? 1 : 0)));
-        } else {
-            if (!PAIR || it % GRP == 0) {
-                if constexpr (KNN_STUDY_NO_BARRIER) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                else wait_dma_barrier();
-            }
+        if (!PAIR || it % GRP == 0) {
+            if constexpr (KNN_STUDY_NO_BARRIER) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            else wait_dma_barrier();
         }
         const uint64_t t1 = now();
         // this tile's terms, for its fast test in the next iteration (the tile is resident:
@@ -980,15 +968,13 @@ int knn_fused_row_bytes(int d) { return d == 64 && KNN_FUSED_AUG64 ? 2 * d + 32 
 FilterPlan knn_fused_plan(int d, int k) {
     const int rb = knn_fused_row_bytes(d);
     const size_t cap = 160 * 1024 - 256;  // room for the kernel's static LDS
-    const int kr = k <= 16 ? KNN_FUSED_SMALL_K_LIST : k <= 32 ? 32 : 0;
+    const int kr = k <= 16 ? 16 : k <= 32 ? 32 : 0;
     auto make = [&](int nw, int rg, int minw, int nbuf) {
         FilterPlan f{nw, 0, rg, minw, nbuf, 32 * nw, fused_lds_of(rb, k, nw, rg, nbuf, kr == 0)};
         f.kr = kr;
         return f;
     };
     if (kr == 0 && d == 64 && fused_lds_of(rb, k, 4, 2, 2, true) <= cap / 2) return make(4, 2, 2, 2);
-    if (KNN_FUSED_QUADS && kr > 0 && fused_lds_of(rb, k, 8, 2, 8, false) <= cap) return make(8, 2, 2, 8);
-    if (KNN_FUSED_DEEP && kr > 0 && fused_lds_of(rb, k, 8, 2, 6, false) <= cap) return make(8, 2, 2, 6);
     if (fused_lds_of(rb, k, 8, 2, 4, kr == 0) <= cap) return make(8, 2, 2, 4);
     if (fused_lds_of(rb, k, 8, 2, 2, kr == 0) <= cap) return make(8, 2, 2, 2);
     if (fused_lds_of(rb, k, 8, 1, 2, kr == 0) <= cap) return make(8, 1, 2, 2);
@@ -999,12 +985,6 @@ template <int RB, int KR>
 static const void* fused_fn_k(const FilterPlan& f) {
 #define KNN_FUSED_FN(NB, NW, RG) reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, NB, NW, RG, KR>)
     if constexpr (KR > 0) {
-        if constexpr (KNN_FUSED_QUADS) {
-            if (f.nbuf == 8) return KNN_FUSED_FN(8, 8, 2);
-        }
-        if constexpr (KNN_FUSED_DEEP) {
-            if (f.nbuf == 6) return KNN_FUSED_FN(6, 8, 2);
-        }
         return KNN_FUSED_FN(4, 8, 2);  // register lists always fit the pairs shape
     } else {
         if (f.nw == 4) return KNN_FUSED_FN(2, 4, 2);
@@ -1015,8 +995,7 @@ static const void* fused_fn_k(const FilterPlan& f) {
 }
 template <int RB>
 static const void* fused_fn(const FilterPlan& f) {
-    return f.kr == 16 ? fused_fn_k<RB, 16>(f) : f.kr == 8 ? fused_fn_k<RB, 8>(f) : f.kr == 32 ? fused_fn_k<RB, 32>(f)
-                                                                                   : fused_fn_k<RB, 0>(f);
+    return f.kr == 16 ? fused_fn_k<RB, 16>(f) : f.kr == 32 ? fused_fn_k<RB, 32>(f) : fused_fn_k<RB, 0>(f);
 }
 
 static const void* fused_ptr(int d, const FilterPlan& f) {
@@ -1036,7 +1015,7 @@ hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st) {
     if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != ld || a.ld_q != ld || !a.qstat)
         return hipErrorInvalidValue;
     if (f.kr > 0 && !(f.nw == 8 && f.rg == 2 &&
-                      (f.nbuf == 4 || (KNN_FUSED_QUADS && f.nbuf == 8) || (KNN_FUSED_DEEP && f.nbuf == 6))))
+                      f.nbuf == 4))
         return hipErrorInvalidValue;  // (fused_fn_k)
     void* args[] = {const_cast<GemmFilterArgs*>(&a)};
     const dim3 grid((unsigned)(a.g2 < 0 ? (int64_t)a.n_qtiles * a.nseg : (int64_t)a.p1_blocks + a.g2));

@@ -61,38 +61,12 @@
 #define KNN_FUSED_KSTEP_ORDER() __builtin_amdgcn_sched_barrier(0)
 #endif
 
-// Register lists for k <= 16 (knn_fused_plan): 16 = one exact list per query shared by its two
-// lanes (both insert both values); 8 = the per-half lists of k <= 32 with 8 entries (each lane
-// inserts only its own value; a looser bound).  KNN_STUDY_HALF_LISTS selects 8.
-#ifdef KNN_STUDY_HALF_LISTS
-#define KNN_FUSED_SMALL_K_LIST 8
-#else
-#define KNN_FUSED_SMALL_K_LIST 16
-#endif
-
-// Tile groups of the register-list shapes (knn_fused_plan): pairs (four buffers, one barrier per
-// two tiles); KNN_STUDY_QUADS: quads where the LDS holds eight buffers (d <= 128), one barrier
-// per four tiles.
-#ifdef KNN_STUDY_QUADS
-#define KNN_FUSED_QUADS 1
-#else
-#define KNN_FUSED_QUADS 0
-#endif
-
 // KNN_STUDY_STAMPS: per-wave shader-clock stamps of the fused filter's loop (barrier wait, step,
 // slow path), summed over the launch into a device array (knn_debug_stamps).  Timing study only.
 #ifdef KNN_STUDY_STAMPS
 #define KNN_FUSED_STAMPS 1
 #else
 #define KNN_FUSED_STAMPS 0
-#endif
-
-// KNN_STUDY_DEEP: pairs with six buffers, the DMA two pairs ahead and counted vmcnt waits
-// (knn_fused_plan, register-list shapes with d <= 128).
-#ifdef KNN_STUDY_DEEP
-#define KNN_FUSED_DEEP 1
-#else
-#define KNN_FUSED_DEEP 0
 #endif
 
 // KNN_STUDY_AUG64: d = 64 keeps the norm in an augmented k-step (2d + 32 bytes per row) instead
@@ -103,11 +77,3 @@
 #define KNN_FUSED_AUG64 0
 #endif
 
-
-// KNN_STUDY_EARLY_DMA: the step's DMA pieces in its first k-steps (piece i in k-step i) instead
-// of spread over the step.
-#ifdef KNN_STUDY_EARLY_DMA
-#define KNN_FUSED_EARLY_DMA 1
-#else
-#define KNN_FUSED_EARLY_DMA 0
-#endif
