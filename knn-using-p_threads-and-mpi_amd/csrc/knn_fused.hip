@@ -25,7 +25,11 @@
 #include "knn_study.h"
 
 // Constants of the filter (each measured against its alternatives; DESIGN.md "Filter studies")
+#ifndef KNN_STUDY_PF
 static constexpr int FUSED_PF = 6;            // A-fragment prefetch depth, in MFMAs
+#else
+static constexpr int FUSED_PF = KNN_STUDY_PF;  // (study builds pf4 / pf8)
+#endif
 static constexpr int FUSED_DEFER_EVERY = 64;  // 8-wave heap shapes: tiles between flushes of the queued values
 static constexpr int FUSED_SHARE_EVERY = 64;  // tiles between threshold exchanges of a query's pieces (gthr)
 static constexpr int FUSED_RQ = 4;            // queued passing values per lane (heap shapes)
