@@ -99,6 +99,41 @@ __device__ __forceinline__ float direct_dist_batched(const float* q, const E* __
     }
     return sum;
 }
+// The same distance with G lanes per row (the rescore when m * G <= 64 survivors, G = d / 32):
+// lane p of a group loads features [32p, 32p + 32) in one batch and squares them, then the sum
+// runs through the group in order -- lane p continues lane p-1's partial sum -- so every
+// addition happens in direct_dist's order and the total (in lane G-1 of the group) has its
+// bits.  One memory round trip per row instead of d / 32.  Every lane of the wave calls it
+// (the hand-off is a shuffle); t is 4-element aligned.
+template <typename E>
+__device__ __forceinline__ float direct_dist_grouped(const float* q, const E* __restrict__ t, bool act,
+                                                     int p, int G) {
+    float sq[32];  // unset in an inactive group, whose sum nobody reads
+    if (act) {
+        float4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = load4(t + 32 * p + 4 * j);
+        const float* qp = q + 32 * p;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            float d0 = qp[4 * j + 0] - v[j].x; sq[4 * j + 0] = d0 * d0;
+            float d1 = qp[4 * j + 1] - v[j].y; sq[4 * j + 1] = d1 * d1;
+            float d2 = qp[4 * j + 2] - v[j].z; sq[4 * j + 2] = d2 * d2;
+            float d3 = qp[4 * j + 3] - v[j].w; sq[4 * j + 3] = d3 * d3;
+        }
+    }
+    float sum = 0.0f;
+    for (int j = 0; j < G; j++) {
+        const float in = __shfl_up(sum, 1);
+        if (p == j) {
+            float s = j ? in : 0.0f;
+#pragma unroll
+            for (int i = 0; i < 32; i++) s = s + sq[i];
+            sum = s;
+        }
+    }
+    return sum;
+}
 #pragma clang fp contract(on)
 
 // ---------------------------------------------------------------------------------
@@ -1112,6 +1147,10 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
     uint32_t* su = reinterpret_cast<uint32_t*>(my + a.q_lds_bytes + a.c_lds_bytes);
     const int64_t q = (int64_t)blockIdx.x * 4 + wave;
     if (q >= a.nq) return;
+    // sub-slice fills: lane sg < nseg holds slice sg's; inclusive prefix over lanes 0..15.
+    // Read before the gate and status words (allocated either way), so the three loads
+    // share one round trip.
+    const int cs = lane < a.nseg ? a.cnt[(int64_t)lane * a.nq + q] : 0;
     if (a.gate && *a.gate == 0) return;  // a gated stage (AUTO's re-run) that is not taken
     if (*a.status & KNN_STATUS_GEMM_UNSAFE) {
         // a norm too large for the certificate: every query takes the exact scan
@@ -1121,8 +1160,6 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
     const int k = a.k;
     const E* train = reinterpret_cast<const E*>(a.train);
     const E* test = reinterpret_cast<const E*>(a.test);
-    // sub-slice fills: lane sg < nseg holds slice sg's; inclusive prefix over lanes 0..15
-    const int cs = lane < a.nseg ? a.cnt[(int64_t)lane * a.nq + q] : 0;
     const bool overflow = __ballot(cs > a.cap_seg) != 0ull;
     int incl = cs;
 #pragma unroll
@@ -1194,11 +1231,18 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
     // the threshold: the smallest x with #{U <= x} >= k, or any x above it -- every x >= it
     // is a valid bound (it only admits more survivors) -- so the bisection stops at 2^10
     // ordered-float steps (2^-13 relative), far inside the certificate's band
+    // the register-resident batches count from their own U bits (no LDS round trip per round)
+    uint32_t ur[RC];
+#pragma unroll
+    for (int i = 0; i < RC; i++) ur[i] = (i < nreg && lane + 64 * i < total) ? f2o(cr[i].U) : 0xffffffffu;
     uint32_t lo = umin, hi = umax;
     while (hi - lo > 1024u) {
         const uint32_t mid = lo + ((hi - lo) >> 1);
         int c = 0;
-        for (int i = 0; i < nreg; i++) {
+#pragma unroll
+        for (int i = 0; i < RC; i++)
+            if (i < nreg) c += __popcll(__ballot(lane + 64 * i < total && ur[i] <= mid));
+        for (int i = RC; i < nreg; i++) {
             const int e = lane + 64 * i;
             // position() shuffles across the wave: every lane calls it (wave-uniform branch)
             const int64_t o = 64 * i + 63 >= su_cap ? position(e) : 0;
@@ -1251,10 +1295,20 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
         // dependent label read after the selection)
         const int lab = lane < m ? a.labels[t] : -1;
         u64 key = KEY_NONE;
-        if (lane < m) {
+        // few survivors: G = d / 32 lanes per row, each row read in one round trip
+        const int G = a.d >> 5;
+        const bool mis = lane < m && ((uintptr_t)(train + (int64_t)t * a.ld_t) & (4 * sizeof(E) - 1)) != 0;
+        // (k <= 32 implies R == 1: the larger lists' instances do not carry its registers)
+        if (R == 1 && (a.d & 31) == 0 && G >= 2 && m * G <= 64 && !__ballot(mis)) {
+            const int r = lane / G, p = lane - r * G;
+            const uint32_t tr = (uint32_t)__shfl((int)t, r < m ? r : 0);
+            const float part = direct_dist_grouped(qs, train + (int64_t)tr * a.ld_t, r < m, p, G);
+            const float dist = __shfl(part, (lane < m ? lane : 0) * G + G - 1);
+            if (lane < m) key = make_key(dist, t);
+        } else if (lane < m) {
             key = make_key(direct_dist_batched(qs, train + (int64_t)t * a.ld_t, a.d), t);
-            if (key == KEY_NONE) key = 0xffffffff00000000ull | t;
         }
+        if (lane < m && key == KEY_NONE) key = 0xffffffff00000000ull | t;
         int rank = 0;
         for (int jj = 0; jj < m; jj++) {
             const u64 kj = ((u64)__builtin_amdgcn_readlane((uint32_t)(key >> 32), jj) << 32) |
