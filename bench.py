@@ -52,6 +52,7 @@ CONFIGS = {
     "C1": (4_000_000, 1_000_000, 256, 100, 10, 3, "strong", "bf16", "train"),
     "L": (30_803, 1_718, 11, 5, 10, 0, "strong", "f32", "arff"),
 }
+DEFAULT_STEPS = {"A": 200, "B": 10, "C": 2, "C1": 3, "L": 50}
 ARFF_L = ("tests/data/large-train.arff", "tests/data/large-test.arff", "tests/golden/pred_large_k5.txt")
 METRIC = "distance pairs/sec + queries/sec at 1/2/4/8 GPUs; accuracy bit-match"
 MFMA_PEAK_TFLOPS = {  # MI355X_MICROARCH.md, dense
@@ -281,8 +282,10 @@ def pmc_traffic(config):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    # default K per workload: a timed region of about 5 s (A's step is ~25 ms), long enough for
+    # an outside sampler of GPU activity to see the run
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default: per config)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default: per config)")
     ap.add_argument("--config", default="A", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--weak", action="store_true",
@@ -295,6 +298,10 @@ def main():
     ap.add_argument("--nt", type=int, default=0, help="override train rows (kernel studies)")
     ap.add_argument("--nq", type=int, default=0, help="override query rows (kernel studies)")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = DEFAULT_STEPS[args.config]
+    if args.warmup is None:
+        args.warmup = 3 if args.config == "A" else 1
 
     import torch
     import torch.distributed as dist
