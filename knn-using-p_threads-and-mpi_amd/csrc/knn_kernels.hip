@@ -500,37 +500,66 @@ __global__ __launch_bounds__(256) void k_row_norms(const E* __restrict__ x, int6
     // on a norm (d u relative) holds for any order.
     float s = 0.0f, se = 0.0f, sr = 0.0f;
     const int g = lane >> 4, l16 = lane & 15;
-    for (int r4 = 0; r4 < 16; r4++) {
-        const int64_t row = r0 + 4 * r4 + g;
-        float a = 0.0f, ae = 0.0f, ar = 0.0f;
-        auto acc = [&](float v) __attribute__((always_inline)) {
-            a = fmaf(v, v, a);
-            if (rstat) {
-                const float rv = __uint_as_float(bf16_rne(oscale * v) << 16) * inv;
-                const float e = v - rv;
-                ae = fmaf(e, e, ae);
-                ar = fmaf(rv, rv, ar);
-            }
-        };
-        if (row < n) {
-            const E* xr = x + row * ld;
-            int i = 4 * l16;
-            for (; i + 4 <= d; i += 64) {
-                const float4 v = load4(xr + i);
-                acc(v.x); acc(v.y); acc(v.z); acc(v.w);
-            }
-            for (int t = (d & ~3) + l16; t < d; t += 16) acc(widen(xr[t]));  // the d % 4 tail
+    float a, ae, ar;
+    auto acc = [&](float v) __attribute__((always_inline)) {
+        a = fmaf(v, v, a);
+        if (rstat) {
+            const float rv = __uint_as_float(bf16_rne(oscale * v) << 16) * inv;
+            const float e = v - rv;
+            ae = fmaf(e, e, ae);
+            ar = fmaf(rv, rv, ar);
         }
+    };
+    // the round's sums to their rows: lane l takes row l = 4 r4 + (l & 3) from lane 16 (l & 3)
+    auto finish_round = [&](int r4) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 8; j > 0; j >>= 1) {
             a += __shfl_xor(a, j);
             if (rstat) { ae += __shfl_xor(ae, j); ar += __shfl_xor(ar, j); }
         }
-        // lane l takes row l = 4 r4 + (l & 3) from lane 16 (l & 3) of this round
         const float va = __shfl(a, 16 * (lane & 3));
         const float vae = rstat ? __shfl(ae, 16 * (lane & 3)) : 0.0f;
         const float var = rstat ? __shfl(ar, 16 * (lane & 3)) : 0.0f;
         if ((lane >> 2) == r4) { s = va; se = vae; sr = var; }
+    };
+    if (d % 4 == 0 && d <= 256) {
+        // four rounds' loads (up to 16 float4 per lane) in flight before their sums, instead of
+        // one load per round trip; the zero padding adds exact zeros, so the sums are the
+        // loop's below bit for bit
+        for (int r4 = 0; r4 < 16; r4 += 4) {
+            float4 v[4][4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int64_t row = r0 + 4 * (r4 + u) + g;
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const int i = 4 * l16 + 64 * c;
+                    v[u][c] = (row < n && i + 4 <= d) ? load4(x + row * ld + i) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                a = 0.0f; ae = 0.0f; ar = 0.0f;
+#pragma unroll
+                for (int c = 0; c < 4; c++) { acc(v[u][c].x); acc(v[u][c].y); acc(v[u][c].z); acc(v[u][c].w); }
+                finish_round(r4 + u);
+            }
+        }
+    } else {
+        for (int r4 = 0; r4 < 16; r4++) {
+            const int64_t row = r0 + 4 * r4 + g;
+            a = 0.0f; ae = 0.0f; ar = 0.0f;
+            if (row < n) {
+                const E* xr = x + row * ld;
+                int i = 4 * l16;
+                for (; i + 4 <= d; i += 64) {
+                    const float4 v = load4(xr + i);
+                    acc(v.x); acc(v.y); acc(v.z); acc(v.w);
+                }
+                for (int t = (d & ~3) + l16; t < d; t += 16) acc(widen(xr[t]));  // the d % 4 tail
+            }
+            finish_round(r4);
+        }
     }
     if (r < n) {
         out[r] = s;
@@ -551,7 +580,12 @@ __global__ __launch_bounds__(256) void k_row_norms(const E* __restrict__ x, int6
             mr = fmaxf(mr, __shfl_xor(mr, j));
         }
         if ((threadIdx.x & 63) == 0) {
-            if (maxo) atomicMax(maxo, f2o(m));
+            // one word for the whole launch: the atomic only when it can raise the maximum (a
+            // stale read is never above the stored value, so nothing larger is skipped)
+            if (maxo) {
+                const uint32_t mo = f2o(m);
+                if (mo > __hip_atomic_load(maxo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(maxo, mo);
+            }
             if (tstat && r < n) tstat[r >> 6] = make_float4(m, me, mr, 0.0f);
         }
     }
