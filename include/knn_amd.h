@@ -66,8 +66,12 @@ typedef enum {
 /* knn_opts.flags */
 #define KNN_OPT_CACHE_TRAIN 1  /* knn_predict keeps the device copy of train across calls, keyed
                                   by (feat, labels, n, d, ld, dtype) and the generation set by
-                                  knn_set_generation: a caller that rewrites a train buffer in
-                                  place bumps the generation */
+                                  knn_set_generation; every entry point also keeps the train-side
+                                  operands of the bf16 MFMA filter (train norms, tile statistics,
+                                  bf16 tile blocks) across calls, keyed by (feat, n, d, ld, dtype,
+                                  filter tile height) and the generation -- a caller that rewrites
+                                  a train buffer in place (or frees it and reuses the address)
+                                  bumps the generation */
 
 /* Context options.  One context drives one device (a compute stream and a copy stream). */
 typedef struct {
@@ -108,8 +112,8 @@ void knn_destroy(knn_ctx* ctx);
 /* Text of the last error on this context ("" if none). */
 const char* knn_last_error(const knn_ctx* ctx);
 
-/* Invalidates cached train uploads (KNN_OPT_CACHE_TRAIN): the cache key includes this
- * generation.  The reference has no counterpart (every KNN() call re-reads ArffData,
+/* Invalidates cached train uploads and cached train-side filter operands
+ * (KNN_OPT_CACHE_TRAIN): both cache keys include this generation.  The reference has no counterpart (every KNN() call re-reads ArffData,
  * main.cpp:40-43). */
 knn_status knn_set_generation(knn_ctx* ctx, uint64_t generation);
 
@@ -164,6 +168,9 @@ knn_status knn_predict_device(knn_ctx* ctx, const knn_dataset* train, const knn_
  * after an all-to-all over the ranks that own the shards), into each query's k nearest
  * by (distance, global index) -- the reference's tie rule over the whole train set --
  * and votes (smallest label on ties).  d_dist / d_idx (optional) receive [nq][k].
+ * Each source list must ascend by (distance, index) with -1 padding last, as
+ * knn_shard_topk_device writes it: the merge reads a list in sorted runs and stops at the
+ * first run that cannot enter the top k.  A descent inside what it reads gives KNN_EINVAL.
  * KNN_ERANGE if some query has fewer than k neighbours over all shards.
  */
 knn_status knn_shard_topk_device(knn_ctx* ctx, const knn_dataset* train_shard, const knn_dataset* test,
@@ -188,9 +195,13 @@ knn_status knn_merge_vote_device(knn_ctx* ctx, int32_t nsrc, int64_t nq, int32_t
  *     by (distance, global index) -- the reference's lower-index tie rule over the whole
  *     train set -- and votes.  d_pred (and optional d_dist / d_idx [owned][k]) receive the
  *     owned queries' results.  Collective: every rank calls it with the same test set and k.
- *     A failure local to one rank (memory, its shard's arguments) is voted on by every rank
- *     (one max-allreduce) before the exchange: the failing rank returns its own status, its
- *     peers KNN_ERCCL, and no rank is left waiting inside the exchange.  With profile = 1 the
+ *     A failure local to one rank (memory, its shard's arguments, a HIP error that leaves the
+ *     device usable) is voted on by every rank (one max-allreduce of a preset device word)
+ *     before the exchange: the failing rank returns its own status, its peers KNN_ERCCL, and
+ *     no rank is left waiting inside the exchange.  A failure of a collective itself (e.g. after
+ *     a device fault) aborts the communicator (ncclCommAbort): that rank returns KNN_ERCCL,
+ *     every later call on the communicator fails, and peers inside the collective are released
+ *     by their own RCCL / watchdog timeout.  With profile = 1 the
  *     context's stage times hold the shard's stages, "exchange" and "merge_vote".
  *   knn_shard_range: the reference's contiguous split with the remainder on the last worker
  *     (multi-thread.cpp:154-158, mpi.cpp:141-170).
@@ -221,8 +232,9 @@ int32_t knn_stage_times(const knn_ctx* ctx, const char** names, float* ms, int32
  * filter ran, 0 = fp32, 1 = bf16, 2 = bf16 hi/lo split of fp32, 3 = bf16 rounding of
  * fp32), [4] 1 when AUTO re-ran the call with the split filter, [5] 1 when the filter
  * ran with the train norm folded into the MFMA (the fused-norm bf16 filter), [6] train
- * bytes and [7] query bytes a knn_predict call copied host -> device.  Returns the number
- * written (<= 8). */
+ * bytes and [7] query bytes a knn_predict call copied host -> device, [8] 1 when the
+ * filter's train-side operands came from the KNN_OPT_CACHE_TRAIN cache (no train norm or
+ * tile-block pass ran).  Returns the number written (<= 9). */
 int32_t knn_last_stats(const knn_ctx* ctx, int64_t* out, int32_t n);
 
 /*

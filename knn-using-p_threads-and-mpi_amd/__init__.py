@@ -301,6 +301,13 @@ class Context:
         # the next call replaces them, so no later array can be allocated at a cached address
         # (_dataset copies inputs of another dtype or layout into temporaries)
         self._train_key = None
+        # device calls under cache_train: the train tensor whose filter operands the library
+        # keeps (knn_predict_device / knn_shard_topk_device), and its torch version counter --
+        # a different tensor or an in-place write bumps the library's generation, and holding
+        # the tensor keeps its address from being reused while it is cached
+        self._dev_train = None
+        self._generation = 0
+        self.device = int(device)
         h = ctypes.c_void_p()
         st = self.lib.knn_create(ctypes.byref(h), ctypes.byref(opts))
         if st != KNN_OK:
@@ -341,21 +348,45 @@ class Context:
                                          q_begin, q_end, _ptr(pred), _ptr(dist), _ptr(idx)))
         return (pred, dist, idx) if topk else pred
 
+    def _stream(self, stream, tensor):
+        """_stream_arg, after checking that the tensor lives on this context's device (a call
+        on another device's stream fails inside HIP with an unhelpful error)."""
+        if tensor is not None and getattr(tensor, "is_cuda", False) and tensor.device.index != self.device:
+            raise KnnError(KNN_EINVAL, f"tensor on cuda:{tensor.device.index}, context on device {self.device}")
+        return _stream_arg(stream, tensor)
+
+    def _note_train(self, train):
+        """cache_train: bump the generation when the train tensor is another one or was written
+        in place since the last device call (torch's version counter)."""
+        if not self.cache_train:
+            return
+        key = (train.data_ptr(), tuple(train.shape), train._version)
+        if self._dev_train is None or self._dev_train[0] is not train or self._dev_train[1] != key:
+            self.set_generation(self._generation + 1)
+            self._dev_train = (train, key)
+
     def predict_device(self, train, labels, test, k, num_classes, pred, dist=None, idx=None,
                        stream=None, d=None):
         """Device tensors (torch, on this context's device) in and out (knn_predict_device).
-        train/test: [n][ld] float32 contiguous; labels/pred/idx int32; dist float32."""
+        train/test: [n][ld] float32 contiguous; labels/pred/idx int32; dist float32.
+        With cache_train the train-side filter operands are kept across calls on the same,
+        unmodified train tensor (rewrites through torch are seen; after writing it by other
+        means call set_generation)."""
+        self._stream(None, train)
+        self._note_train(train)
         tr = _device_dataset(train, labels, d)
         te = _device_dataset(test, None, d)
         _outputs(te.n, k, pred, dist, idx)
         self._check(self.lib.knn_predict_device(
             self.h, ctypes.byref(tr), ctypes.byref(te), k, num_classes, pred.data_ptr(),
             None if dist is None else dist.data_ptr(), None if idx is None else idx.data_ptr(),
-            _stream_arg(stream, test)))
+            self._stream(stream, test)))
 
     def shard_topk_device(self, train, labels, test, k, num_classes, idx_base, rec, stream=None, d=None):
         """Exact k nearest rows of one train shard for every query (knn_shard_topk_device).
         rec: int32 device tensor [nq][3][k] <- (dist bits, idx_base + row, label), ascending."""
+        self._stream(None, train)
+        self._note_train(train)
         tr = _device_dataset(train, labels, d)
         te = _device_dataset(test, None, d)
         if tuple(rec.shape) != (test.shape[0], 3, k):
@@ -364,7 +395,7 @@ class Context:
         _check_tensor(rec, "rec", torch.int32)
         self._check(self.lib.knn_shard_topk_device(
             self.h, ctypes.byref(tr), ctypes.byref(te), k, num_classes, idx_base, rec.data_ptr(),
-            _stream_arg(stream, test)))
+            self._stream(stream, test)))
 
     def merge_vote_device(self, rec, k, num_classes, pred, dist=None, idx=None, stream=None):
         """Merge nsrc per-shard neighbour lists rec [nsrc][nq][3][k] and vote (knn_merge_vote_device)."""
@@ -377,7 +408,7 @@ class Context:
         self._check(self.lib.knn_merge_vote_device(
             self.h, nsrc, nq, k, num_classes, rec.data_ptr(), pred.data_ptr(),
             None if dist is None else dist.data_ptr(), None if idx is None else idx.data_ptr(),
-            _stream_arg(stream, rec)))
+            self._stream(stream, rec)))
 
     def generate(self, feat, labels, row0, d, kind, seed, stream_id, num_classes, dtype=None,
                  stream=None):
@@ -387,7 +418,9 @@ class Context:
         self._check(self.lib.knn_generate(
             self.h, feat.data_ptr(), None if labels is None else labels.data_ptr(), row0,
             feat.shape[0], d, feat.shape[1], dtype, kind, seed, stream_id, num_classes,
-            _stream_arg(stream, feat)))
+            self._stream(stream, feat)))
+        if self._dev_train is not None and self._dev_train[0] is feat:
+            self._dev_train = None  # written behind torch's back: the next call bumps the generation
 
     def confusion_matrix_device(self, pred, labels, num_classes, cm=None, stream=None):
         """computeConfusionMatrix / computeAccuracy (main.cpp:87-112) on device tensors:
@@ -400,7 +433,7 @@ class Context:
         corr = torch.zeros(1, dtype=torch.int64, device=pred.device)
         self._check(self.lib.knn_confusion_matrix_device(
             self.h, pred.data_ptr(), labels.data_ptr(), pred.shape[0], num_classes, cm.data_ptr(),
-            corr.data_ptr(), _stream_arg(stream, pred)))
+            corr.data_ptr(), self._stream(stream, pred)))
         n = pred.shape[0]
         return cm, float(np.float32(int(corr.item())) / np.float32(n)) if n else float("nan")
 
@@ -413,12 +446,13 @@ class Context:
         a, b = a.contiguous(), b.contiguous()
         out = torch.empty((32, 32), dtype=torch.float32, device=a.device)
         self._check(self.lib.knn_mfma_probe_bf16(self.h, a.data_ptr(), b.data_ptr(), a.shape[1], out.data_ptr(),
-                                                 _stream_arg(stream, a)))
+                                                 self._stream(stream, a)))
         return out
 
     def set_generation(self, generation):
-        """Invalidate cached train uploads (knn_set_generation)."""
+        """Invalidate cached train uploads and train-side filter operands (knn_set_generation)."""
         self._check(self.lib.knn_set_generation(self.h, generation))
+        self._generation = int(generation)
 
     def stage_times(self):
         names = (ctypes.c_char_p * 256)()
@@ -431,11 +465,12 @@ class Context:
         return out
 
     def stats(self):
-        v = (ctypes.c_int64 * 8)()
-        self.lib.knn_last_stats(self.h, v, 8)
+        v = (ctypes.c_int64 * 9)()
+        self.lib.knn_last_stats(self.h, v, 9)
         return {"candidates": v[0], "fallback_queries": v[1], "train_segments": v[2],
                 "filter_operands": FILTER_OPERANDS.get(v[3], v[3]), "rerun_split": bool(v[4]),
-                "fused_norm": bool(v[5]), "h2d_train_bytes": v[6], "h2d_query_bytes": v[7]}
+                "fused_norm": bool(v[5]), "h2d_train_bytes": v[6], "h2d_query_bytes": v[7],
+                "train_operands_cached": bool(v[8])}
 
 
 def comm_unique_id():
@@ -497,6 +532,8 @@ class Comm:
                               stream=None, d=None):
         """knn_predict_train_sharded: this rank's train shard (global rows [idx_base, ...)) and
         every query in, the owned queries' (shard_range) predictions out."""
+        self.ctx._stream(None, shard)
+        self.ctx._note_train(shard)
         tr = _device_dataset(shard, labels, d)
         te = _device_dataset(test, None, d)
         q0, q1 = shard_range(te.n, self.nranks, self.rank)
@@ -504,7 +541,7 @@ class Comm:
         st = self.lib.knn_predict_train_sharded(
             self.ctx.h, self.h, ctypes.byref(tr), idx_base, ctypes.byref(te), k, num_classes, pred.data_ptr(),
             None if dist is None else dist.data_ptr(), None if idx is None else idx.data_ptr(),
-            _stream_arg(stream, test))
+            self.ctx._stream(stream, test))
         if st != KNN_OK:
             raise KnnError(st, self.lib.knn_last_error(self.ctx.h).decode())
         return q0, q1

@@ -65,6 +65,17 @@ struct knn_ctx {
     DBuf tmax;              // fused filter: per-64-row train stats {max tn, max |t - rt|, max |rt|, 0}
     DBuf cursor;            // fused filter: per-XCD scan cursors (64-row units; performance hint only)
     DBuf qstat;             // fused filter: per-query {|q|, |q - rq|} upper bounds
+    DBuf tblk;              // fused filter: train tile blocks [bn rows rn(t) | bn norms | tile stats]
+    DBuf tctrl;             // the train norms' share of the status word: [unsafe bits, 0, max norm, 0]
+    // train-side operands of the fused filter (tnorm, tnp, tmax, tblk, tctrl) kept across calls
+    // under KNN_OPT_CACHE_TRAIN, keyed by the train view, the tile height and the generation;
+    // epoch = the upload count of knn_predict's own train buffer (its pointer does not change)
+    struct { const void* feat; int64_t n; int d, ld, dtype, bn; uint64_t gen, epoch; bool valid; }
+        tprep{nullptr, 0, 0, 0, 0, 0, 0, 0, false};
+    uint64_t train_epoch = 0;
+    // the same for the non-fused GEMM paths' train copy padded to the 64-row grid (pad_t)
+    struct { const void* feat; int64_t n; int d, ld, dtype; uint64_t gen, epoch; bool valid; }
+        tpad{nullptr, 0, 0, 0, 0, 0, 0, false};
     int rescore_su = 0;  // test hook KNN_RESCORE_SU: the rescore's LDS staging size (0 = sized)
     // host-API staging (device copies of host inputs / outputs)
     DBuf h_train, h_labels, h_test, h_pred, h_dist, h_idx;
@@ -86,8 +97,9 @@ struct knn_ctx {
     std::vector<Stage> stages;
     std::vector<float> stage_ms;
     std::vector<const char*> stage_names;
-    int64_t stats[8] = {0, 0, 0, -1, 0, 0, 0, 0};  // candidates, fallback queries, segments, filter operand
-                                                   // type, rerun, fused, train / query H2D bytes
+    int64_t stats[9] = {0, 0, 0, -1, 0, 0, 0, 0, 0};  // candidates, fallback queries, segments, filter
+                                                      // operand type, rerun, fused, train / query H2D
+                                                      // bytes, train-side filter operands from the cache
     int64_t rerun_stats[3] = {0, -1, 0};    // segments, operand type, fused of AUTO's gated split re-run
     int num_cus = 256;
 };
@@ -206,6 +218,8 @@ void collect_stages(knn_ctx* c) {
 knn_status check_status(knn_ctx* c, const int32_t* ctrl) {
     const int32_t status = ctrl[0];
     if (status & KNN_STATUS_BAD_LABEL) return fail(c, KNN_EINVAL, "a train label is outside [0, num_classes)");
+    if (status & KNN_STATUS_UNSORTED)
+        return fail(c, KNN_EINVAL, "merge: a source neighbour list is not ascending by (distance, index)");
     if (status & KNN_STATUS_TOO_FEW) return fail(c, KNN_ERANGE, "fewer than k train rows have a finite distance (< FLT_MAX)");
     return KNN_OK;
 }
@@ -315,9 +329,10 @@ void certificate(int d, int felem, float* coef, float* eta) {
     }
 }
 
-// Fused-norm filter (knn_fused.hip): y = fl_mfma(sum -2 rq_i rt_i + tn_hi + tn_mid + tn_lo)
-// (d = 64: the norm split over an augmented k-step), or y = fl_mfma(tn + sum -2 rq_i rt_i)
-// (d >= 128: the fp32 norm is the first MFMA's C operand), G = fl(qn + y), Delta = coef (qn +
+// Fused-norm filter (knn_fused.hip): y = fl_mfma(tn + sum -2 rq_i rt_i) -- the fp32 norm from
+// the tile block's header is the first MFMA's C operand, every d (the KNN_STUDY_AUG64 build
+// splits it over an augmented k-step at d = 64 instead: + tn_hi + tn_mid + tn_lo, the terms
+// the coefficient still covers), G = fl(qn + y), Delta = coef (qn +
 // tn) + eta; rq, rt = the bf16 operands (q, t themselves for bf16 data, rn(q), rn(t) for fp32
 // data).  With N = qn + tn (exact norms):
 //   MFMA accumulation of d + 3 terms (d + 1 with the C-operand norm) at <= 2u per add, terms
@@ -414,11 +429,37 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     } else {
         certificate(d, felem, &coef, &eta);
     }
+    // train-side operands of the fused filter: norms + tile statistics (k_row_norms) and the
+    // tile blocks (k_tn_rows), reused from an earlier call on the same train view when the
+    // context caches train (no train pass at all then; main.cpp:40-43 re-reads every train row
+    // per query, this is the part of that work that depends on train alone)
+    const bool fused_tn = fused && knn_fused_row_bytes(d) == 2 * d;
+    const int bn_f = fused ? 32 * knn_fused_plan(d, k).rg : 0;
+    const bool own_train = tr->feat == c->h_train.p;  // knn_predict's uploaded copy
+    auto& tp = c->tprep;
+    const bool prep_hit = fused_tn && !gate && c->cache_train && tp.valid && tp.feat == tr->feat && tp.n == nt &&
+                          tp.d == d && tp.ld == tr->ld && tp.dtype == dtype && tp.bn == bn_f &&
+                          tp.gen == c->generation && tp.epoch == (own_train ? c->train_epoch : 0);
+    if (fused_tn && !gate) {
+        HIP_OR_FAIL(c, c->tctrl.ensure(4 * sizeof(int32_t)));
+        tp.valid = false;  // (set again below once this call's train pass is enqueued)
+    }
     stage_begin(c, st, gate ? "norms_rerun" : "norms");
-    HIP_OR_FAIL(c, knn_launch_row_norms(tr->feat, dtype, nt, tr->ld, d, c->tnorm.as<float>(),
-                                        c->ctrl.as<int32_t>(), c->ctrl.as<uint32_t>() + 2,
-                                        c->tnp.as<float>(), 1.0f - coef, st, fused ? c->tmax.as<float4>() : nullptr,
-                                        gate));
+    if (fused_tn && !gate) {
+        // train norms into their own status words, then into this call's status word
+        if (!prep_hit) {
+            HIP_OR_FAIL(c, hipMemsetAsync(c->tctrl.p, 0, 4 * sizeof(int32_t), st));
+            HIP_OR_FAIL(c, knn_launch_row_norms(tr->feat, dtype, nt, tr->ld, d, c->tnorm.as<float>(),
+                                                c->tctrl.as<int32_t>(), c->tctrl.as<uint32_t>() + 2,
+                                                c->tnp.as<float>(), 1.0f - coef, st, c->tmax.as<float4>(), nullptr));
+        }
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->ctrl.p, c->tctrl.p, 4 * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    } else {
+        HIP_OR_FAIL(c, knn_launch_row_norms(tr->feat, dtype, nt, tr->ld, d, c->tnorm.as<float>(),
+                                            c->ctrl.as<int32_t>(), c->ctrl.as<uint32_t>() + 2,
+                                            c->tnp.as<float>(), 1.0f - coef, st, fused ? c->tmax.as<float4>() : nullptr,
+                                            gate));
+    }
     // (the fused filter's query operand is rn(-2 q): its rounding is bounded for rn(-2 q) / -2)
     HIP_OR_FAIL(c, knn_launch_row_norms(te->feat, dtype, nq, te->ld, d, c->qnorm.as<float>(),
                                         c->ctrl.as<int32_t>(), nullptr, nullptr, 0.0f, st, nullptr, gate,
@@ -436,23 +477,28 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     const void* ftrain = tr->feat;
     const void* ftest = te->feat;
     int fld_t = tr->ld, fld_q = te->ld;
-    if (fused && knn_fused_row_bytes(d) == 2 * d) {
+    if (fused_tn) {
         // train as tile blocks [bn rows of rn(t) | bn norms | tile statistics] (the
         // filter starts each accumulator from the norms), queries as rn(-2 q) rows; one more
-        // tile of pad blocks past the grid (the filter scans tiles in twos, k_gemm_fused)
-        const int bn = 32 * knn_fused_plan(d, k).rg;
+        // tile of pad blocks past the grid (the filter scans tiles in twos, k_gemm_fused).
+        // The gated split re-run never takes this branch (the fused filter is the first pass).
         const int64_t ntf = ntp + 64;
-        const size_t tb = (size_t)bn * 2 * d + 4 * bn + 16;
-        HIP_OR_FAIL(c, c->split_t.ensure(tb * (size_t)(ntf / bn)));
+        const size_t tb = (size_t)bn_f * 2 * d + 4 * bn_f + 16;
         HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * (size_t)d * nq));
-        stage_begin(c, st, gate ? "aug_rerun" : "aug");
-        HIP_OR_FAIL(c, knn_launch_tn_rows(tr->feat, dtype, ntf, nt, tr->ld, d, c->tnorm.as<float>(), 1.0f,
-                                          c->split_t.p, c->tmax.as<float4>(), bn, st, gate));
+        stage_begin(c, st, "aug");
+        if (!prep_hit) {
+            HIP_OR_FAIL(c, c->tblk.ensure(tb * (size_t)(ntf / bn_f)));
+            HIP_OR_FAIL(c, knn_launch_tn_rows(tr->feat, dtype, ntf, nt, tr->ld, d, c->tnorm.as<float>(), 1.0f,
+                                              c->tblk.p, c->tmax.as<float4>(), bn_f, st, nullptr));
+        }
         HIP_OR_FAIL(c, knn_launch_tn_rows(te->feat, dtype, nq, nq, te->ld, d, nullptr, -2.0f, c->split_q.p, nullptr,
-                                          0, st, gate));
+                                          0, st, nullptr));
         stage_end(c, st);
-        ftrain = c->split_t.p; ftest = c->split_q.p;
+        ftrain = c->tblk.p; ftest = c->split_q.p;
         fld_t = fld_q = d;
+        c->stats[8] = prep_hit ? 1 : 0;
+        if (c->cache_train)
+            tp = {tr->feat, nt, d, tr->ld, dtype, bn_f, c->generation, own_train ? c->train_epoch : 0, true};
     } else if (fused) {
         // (study build KNN_STUDY_AUG64, d = 64) augmented bf16 rows: train [rn(t) | tn split],
         // queries [-2 rn(q) | 1 1 1]
@@ -491,11 +537,20 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         fld_t = fld_q = d;
     } else if (nt % 64) {
         // the caller's rows, copied onto the 64-row tile grid: every tile the filter copies
-        // into LDS is whole (one DMA form, knn_kernels.hip), the pad rows never pass (+inf norms)
+        // into LDS is whole (one DMA form, knn_kernels.hip), the pad rows never pass (+inf norms).
+        // Kept across calls like the fused operands (KNN_OPT_CACHE_TRAIN, same key).
         const size_t es = (size_t)elem_size(dtype), pitch = es * (size_t)tr->ld;
-        HIP_OR_FAIL(c, c->pad_t.ensure(pitch * (size_t)ntp));
-        HIP_OR_FAIL(c, hipMemcpyAsync(c->pad_t.p, tr->feat, pitch * (size_t)nt, hipMemcpyDeviceToDevice, st));
-        HIP_OR_FAIL(c, hipMemsetAsync((unsigned char*)c->pad_t.p + pitch * (size_t)nt, 0, pitch * (size_t)(ntp - nt), st));
+        auto& pk = c->tpad;
+        const uint64_t ep = tr->feat == c->h_train.p ? c->train_epoch : 0;
+        const bool hit = c->cache_train && pk.valid && pk.feat == tr->feat && pk.n == nt && pk.d == d &&
+                         pk.ld == tr->ld && pk.dtype == dtype && pk.gen == c->generation && pk.epoch == ep;
+        pk.valid = false;
+        if (!hit) {
+            HIP_OR_FAIL(c, c->pad_t.ensure(pitch * (size_t)ntp));
+            HIP_OR_FAIL(c, hipMemcpyAsync(c->pad_t.p, tr->feat, pitch * (size_t)nt, hipMemcpyDeviceToDevice, st));
+            HIP_OR_FAIL(c, hipMemsetAsync((unsigned char*)c->pad_t.p + pitch * (size_t)nt, 0, pitch * (size_t)(ntp - nt), st));
+        }
+        if (c->cache_train) pk = {tr->feat, nt, d, tr->ld, dtype, c->generation, ep, true};
         ftrain = c->pad_t.p;
     }
 
@@ -641,7 +696,7 @@ void knn_destroy(knn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (DBuf* b : {&c->tnorm, &c->tnp, &c->qnorm, &c->gthr, &c->cnt, &c->cand,
-                    &c->fb_list, &c->ctrl, &c->scratch, &c->split_t, &c->split_q, &c->pad_t, &c->seg_rec, &c->tmax, &c->qstat, &c->cursor, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
+                    &c->fb_list, &c->ctrl, &c->scratch, &c->split_t, &c->split_q, &c->pad_t, &c->seg_rec, &c->tmax, &c->qstat, &c->tblk, &c->tctrl, &c->cursor, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
                     &c->h_dist, &c->h_idx})
         b->release();
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
@@ -764,7 +819,7 @@ knn_dataset offset_rows(const knn_dataset& x, int64_t r0, int64_t n) {
 
 void reset_stats(knn_ctx* c) {
     c->stages.clear();
-    for (int i = 0; i < 8; i++) c->stats[i] = 0;
+    for (int i = 0; i < 9; i++) c->stats[i] = 0;
     c->stats[3] = -1;
 }
 
@@ -786,8 +841,11 @@ knn_status predict_core(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te
     const int64_t pass = gemm ? std::max<int64_t>(1, c->ws_queries) : te->n;
     for (int64_t q0 = 0; q0 < te->n; q0 += pass) {
         const knn_dataset tq = offset_rows(*te, q0, std::min(pass, te->n - q0));
-        if ((s = predict_enqueue(c, tr, &tq, k, C, offset_out(out, q0), st, algo, nullptr)) != KNN_OK) return s;
-        if ((s = finish_call(c, st)) != KNN_OK) return s;
+        if ((s = predict_enqueue(c, tr, &tq, k, C, offset_out(out, q0), st, algo, nullptr)) != KNN_OK ||
+            (s = finish_call(c, st)) != KNN_OK) {
+            if (s != KNN_EINVAL && s != KNN_ERANGE) c->tprep.valid = c->tpad.valid = false;  // a HIP failure: the operands may be partial
+            return s;
+        }
         pass_stats(c, c->ctrl_host, gemm);
     }
     if (c->profile >= 2 && gemm) {
@@ -813,6 +871,7 @@ knn_status train_device(knn_ctx* c, const knn_dataset* tr, hipStream_t st, knn_d
                      tc.d == tr->d && tc.ld == tr->ld && tc.dtype == tr->dtype && tc.gen == c->generation;
     if (!hit) {
         tc.valid = false;
+        c->train_epoch++;  // the uploaded copy changes: the train-side filter operands of it are stale
         HIP_OR_FAIL(c, c->h_train.ensure(es * (size_t)ldd * tr->n));
         HIP_OR_FAIL(c, c->h_labels.ensure(sizeof(int32_t) * tr->n));
         HIP_OR_FAIL(c, hipMemcpy2DAsync(c->h_train.p, es * ldd, tr->feat, es * tr->ld, es * tr->d, tr->n,
@@ -927,6 +986,7 @@ knn_status knn_predict(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te,
         (void)hipStreamSynchronize(cs);
         (void)hipStreamSynchronize(st);
         c->tcache.valid = false;
+        c->tprep.valid = c->tpad.valid = false;
         return e;
     };
     knn_dataset dtr;
@@ -1021,7 +1081,7 @@ int32_t knn_stage_times(const knn_ctx* c, const char** names, float* ms, int32_t
 
 int32_t knn_last_stats(const knn_ctx* c, int64_t* out, int32_t n) {
     if (!c || !out) return 0;
-    int32_t m = std::min(n, 8);
+    int32_t m = std::min(n, 9);
     for (int32_t i = 0; i < m; i++) out[i] = c->stats[i];
     return m;
 }

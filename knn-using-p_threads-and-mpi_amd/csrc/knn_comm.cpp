@@ -41,6 +41,7 @@ struct Rccl {
     decltype(&ncclGetUniqueId) get_unique_id = nullptr;
     decltype(&ncclCommInitRank) init_rank = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclCommAbort) abort = nullptr;
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclSend) send = nullptr;
@@ -67,6 +68,7 @@ Rccl& rccl() {
         KNN_RCCL_SYM(get_unique_id, "ncclGetUniqueId");
         KNN_RCCL_SYM(init_rank, "ncclCommInitRank");
         KNN_RCCL_SYM(destroy, "ncclCommDestroy");
+        KNN_RCCL_SYM(abort, "ncclCommAbort");
         KNN_RCCL_SYM(group_start, "ncclGroupStart");
         KNN_RCCL_SYM(group_end, "ncclGroupEnd");
         KNN_RCCL_SYM(send, "ncclSend");
@@ -98,8 +100,12 @@ struct knn_comm {
     size_t rec_bytes = 0;
     void* lists = nullptr;
     size_t lists_bytes = 0;
-    int32_t* flag = nullptr;       // device word of the per-call failure vote (allocated at create)
+    // the per-call failure vote, allocated at create: flag[0] receives the max-allreduce of
+    // flag[1] (= 0, this rank succeeded) or flag[2] (= 1, it failed) -- constants written once,
+    // so taking part in the vote needs no copy that could itself fail
+    int32_t* flag = nullptr;
     int32_t* flag_host = nullptr;  // pinned copy of the vote's result
+    bool broken = false;           // aborted after a failed collective: every later call fails
     std::string err;
 };
 
@@ -172,10 +178,15 @@ knn_status knn_comm_create(knn_ctx* ctx, const void* id, int32_t nranks, int32_t
         return KNN_EHIP;
     }
     // the failure vote's words exist before any call, so a call never fails to take part in it
-    if (hipMalloc((void**)&c->flag, sizeof(int32_t)) != hipSuccess ||
+    static const int32_t words[3] = {0, 0, 1};
+    if (hipMalloc((void**)&c->flag, sizeof(words)) != hipSuccess ||
         hipHostMalloc((void**)&c->flag_host, sizeof(int32_t), hipHostMallocDefault) != hipSuccess) {
         knn_comm_destroy(c);
         return KNN_ENOMEM;
+    }
+    if (hipMemcpy(c->flag, words, sizeof(words), hipMemcpyHostToDevice) != hipSuccess) {
+        knn_comm_destroy(c);
+        return KNN_EHIP;
     }
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
@@ -199,7 +210,10 @@ knn_status knn_comm_count(const knn_comm* c, int32_t* nranks) {
 void knn_comm_destroy(knn_comm* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->comm && rccl_ok()) (void)rccl().destroy(c->comm);
+    if (c->comm && rccl_ok()) {
+        if (c->broken && rccl().abort) (void)rccl().abort(c->comm);
+        else (void)rccl().destroy(c->comm);
+    }
     if (c->rec) (void)hipFree(c->rec);
     if (c->lists) (void)hipFree(c->lists);
     if (c->flag) (void)hipFree(c->flag);
@@ -231,21 +245,34 @@ knn_status knn_predict_train_sharded(knn_ctx* ctx, knn_comm* comm, const knn_dat
     if (s == KNN_OK) s = knn_shard_topk_device(ctx, shard, test, k, num_classes, idx_base, (int32_t*)comm->rec, st);
     // 2. every rank votes on whether all shards succeeded (a max-allreduce of one word), so a
     //    rank that failed locally still meets its peers here and all of them return instead of
-    //    one leaving the others blocked inside the exchange
+    //    one leaving the others blocked inside the exchange.  The vote reads a preset device
+    //    word (flag[1] or flag[2]): no copy precedes it.  What the vote cannot cover is a
+    //    failure of the collective itself (e.g. a sticky device fault from step 1 makes RCCL's
+    //    own launch fail): then the communicator is aborted (ncclCommAbort), this rank returns
+    //    KNN_ERCCL, and the communicator fails every later call; peers already inside the
+    //    all-reduce are released only by their own RCCL timeout (NCCL_COMM_BLOCKING /
+    //    the caller's watchdog), since no signal reaches them from a faulted device.
     Rccl& r = rccl();
-    const int32_t mine = s == KNN_OK ? 0 : 1;
-    if (hipMemcpyAsync(comm->flag, &mine, sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
-        r.all_reduce(comm->flag, comm->flag, 1, ncclInt32, ncclMax, comm->comm, st) != ncclSuccess ||
-        hipMemcpyAsync(comm->flag_host, comm->flag, sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
+    auto give_up = [&]() {
+        if (!comm->broken && r.abort) (void)r.abort(comm->comm);
+        comm->broken = true;
         return KNN_ERCCL;
+    };
+    if (comm->broken) return KNN_ERCCL;
+    const int32_t* vote_src = comm->flag + (s == KNN_OK ? 1 : 2);
+    if (r.all_reduce(vote_src, comm->flag, 1, ncclInt32, ncclMax, comm->comm, st) != ncclSuccess) return give_up();
+    if (hipMemcpyAsync(comm->flag_host, comm->flag, sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return give_up();
     if (s != KNN_OK) return s;
     if (*comm->flag_host != 0) return KNN_ERCCL;  // a peer's shard failed
     // 3. all-to-all of the records: rank b receives the rows of its own queries from everyone
+    //    (a failure inside the group still closes it, then aborts: peers must not wait on a
+    //    half-posted exchange)
     int64_t so[1024], sc[1024], ro[1024], rc[1024];
     knn_exchange_layout(nq, k, comm->nranks, comm->rank, so, sc, ro, rc);
     knn_ctx_stage_begin(ctx, st, "exchange");
-    if (r.group_start() != ncclSuccess) return KNN_ERCCL;
+    if (r.group_start() != ncclSuccess) return give_up();
     bool ok = true;
     for (int32_t b = 0; b < comm->nranks && ok; b++) {
         if (sc[b] > 0 && r.send((const int32_t*)comm->rec + so[b], (size_t)sc[b], ncclInt32, b, comm->comm, st) != ncclSuccess)
@@ -254,7 +281,7 @@ knn_status knn_predict_train_sharded(knn_ctx* ctx, knn_comm* comm, const knn_dat
             r.recv((int32_t*)comm->lists + ro[b], (size_t)rc[b], ncclInt32, b, comm->comm, st) != ncclSuccess)
             ok = false;
     }
-    if (r.group_end() != ncclSuccess || !ok) return KNN_ERCCL;
+    if (r.group_end() != ncclSuccess || !ok) return give_up();
     knn_ctx_stage_end(ctx, st);
     // 4. merge + vote of the owned queries (ordered by distance, then global index); the
     //    shard's stage times stay in the context's profile beside the exchange and the merge

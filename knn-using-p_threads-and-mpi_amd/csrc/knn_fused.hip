@@ -1,21 +1,19 @@
 // knn_fused.hip -- the GEMM-form candidate filter on the bf16 MFMA with the train norm
-// folded into the MFMA (gfx950).  DESIGN.md "Fused-norm filter".
+// folded into the MFMA (gfx950).  DESIGN.md "k_gemm_fused".
 //
-// Rows are augmented by 16 bf16 columns (k_aug_rows):
-//   train  [ rn(t_0) .. rn(t_{d-1}) | tn_hi tn_mid tn_lo 0 x 5 | s0 s1 s2 0 x 5 ]   (tn = ||t||^2, fp32)
-//   query  [ -2 rn(q_0) .. -2 rn(q_{d-1}) | 1 1 1 0 x 13 ]
-// where s0..s2 (rows 32i only, else 0) are the 64-row tile's statistics {max tn, max |t - rt|,
-// max |rt|} rounded UP to bf16: they travel into LDS with the tile (no scalar loads in the
-// filter's loop) and multiply the queries' zero columns.
-// so one chain of v_mfma_f32_32x32x16_bf16 over d/16 + 1 k-steps leaves
+// Train operand: tile blocks (k_tn_rows), one per tile of bn rows,
+//   [ bn rows x d bf16 rn(t) | bn fp32 norms tn = ||t||^2 | {max tn, max |t - rt|, max |rt|, 0} ]
+// -- exactly the bytes one tile's LDS-DMA copies.  Query operand: [nq][d] bf16 rn(-2 q).
+// Each accumulator starts from its rows' norms (the first MFMA's C operand), so one chain of
+// v_mfma_f32_32x32x16_bf16 over d/16 k-steps leaves
 //   y = tn - 2 rn(q).rn(t)
 // in the accumulators: the fast test is a v_min3 chain over the 16 values of an
 // accumulator against one per-(query, tile) threshold, with no per-value norm read or
-// fma; the slow path walks the values in a runtime loop with a wave-uniform index (a
-// scalar-indexed register read, no scratch), computes the exact certificate bounds
-//   G = qn + y,  Delta = coef (qn + tn) + eta,  L = G - Delta <= D <= U = G + Delta
+// fma; the slow path takes each lane's passing values, computes the certificate bounds
+//   G = qn + y,  Delta = coef (qn + tmax_tile) + eta + rho,  L = G - Delta <= D <= U = G + Delta
 // (D: the reference's direct-form distance, main.cpp:14-23) and keeps (row, L, U) for
-// the exact rescore (k_rescore) exactly like k_gemm_filter.
+// the exact rescore (k_rescore).  (The KNN_STUDY_AUG64 build keeps the round-2 layout at
+// d = 64: rows augmented by 16 bf16 columns carrying the norm split, k_aug_rows.)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -368,15 +366,20 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     }
     const uint32_t lds_tiles = __builtin_amdgcn_readfirstlane(lds_addr(tiles));
     struct DmaTile { const unsigned char* src; uint32_t lds; };
-    auto dma_desc = [&](int buf, int64_t r0) -> DmaTile {
-        return DmaTile{trainb + (TN ? (r0 / BN) * TB : r0 * ldb), lds_tiles + (uint32_t)(buf * TILE)};
+    // the source of a tile: its block in the train operand (rows are whole 64-row tiles: the
+    // piece's first row and BN are multiples of 64)
+    const int64_t TBR = TN ? TB : (int64_t)BN * ldb;  // operand bytes per tile
+    const unsigned char* piece_src = trainb + (row_begin / BN) * TBR;
+    auto dma_desc = [&](int buf, int t) -> DmaTile {  // logical tile t of the piece
+        int pt = t + rot;
+        pt = pt >= ntiles ? pt - ntiles : pt;
+        return DmaTile{piece_src + (int64_t)pt * TBR, lds_tiles + (uint32_t)(buf * TILE)};
     };
+    // The last piece of a tile is issued whole: its lanes past the header re-read the header's
+    // last slot into the buffer's slack (TILE = DMA_INS KiB), so no piece needs an exec mask.
     auto dma_piece = [&](int i, const DmaTile& d) __attribute__((always_inline)) {
         const int ins = wave + NW * i;
-        if (ins < DMA_INS) {
-            if (ins == DMA_INS - 1 && lane >= FT::LAST_LANES) return;
-            dma16s(doff[i], d.src, d.lds + (uint32_t)ins * 1024u);
-        }
+        if (NW * (i + 1) <= DMA_INS || ins < DMA_INS) dma16s(doff[i], d.src, d.lds + (uint32_t)ins * 1024u);
     };
     // piece i goes out in k-step (i NS) / DMA_PER_WAVE of the step
     auto dma_at = [&](int s, bool on, const DmaTile& d) __attribute__((always_inline)) {
@@ -758,7 +761,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
 #pragma unroll
     for (int p = 0; p < AHEAD; p++)
         if (p < ntiles) {
-            const DmaTile d0 = dma_desc(p, tile_row(p));
+            const DmaTile d0 = dma_desc(p, p);
 #pragma unroll
             for (int i = 0; i < DMA_PER_WAVE; i++) dma_piece(i, d0);
         }
@@ -801,7 +804,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         // landed before this step's barrier, not overwritten before the next one)
         const float2 tm_cur = tile_q(it % NBUF);
         const bool dma_on = !KNN_STUDY_NO_DMA && it + AHEAD < ntiles;
-        const DmaTile dd = dma_desc((it + AHEAD) % NBUF, tile_row(it + AHEAD));
+        const DmaTile dd = dma_desc((it + AHEAD) % NBUF, it + AHEAD);
         const float tf = it > 0 ? tf_of(tm_prev) : -INF;
         const uint32_t uY = step(X, Y, it % NBUF, dma_on, dd, tf, PAIR && it % GRP != 0);
         // PAIR: the pair's next tile is resident since its barrier -- its first fragments are

@@ -7,6 +7,7 @@
 #define KNN_STATUS_TOO_FEW 1       // a query has fewer than k finite distances
 #define KNN_STATUS_BAD_LABEL 2     // a neighbour's label is outside [0, C)
 #define KNN_STATUS_GEMM_UNSAFE 4   // a row norm is too large for the GEMM certificate
+#define KNN_STATUS_UNSORTED 8      // k_merge_vote: a source list read was not ascending by (dist, idx)
 
 // candidate-list capacity per query on the GEMM path (entries = 64 * CAPW)
 #define KNN_RESCORE_CAPW 32
@@ -149,7 +150,8 @@ hipError_t knn_launch_fill_u32(uint32_t* p, int64_t n, uint32_t v, const int32_t
 // AUTO's re-run decision on the device: ctrl[3] = !unsafe && ctrl[1] > limit (and ctrl[1] = 0 then)
 hipError_t knn_launch_rerun_decide(int32_t* ctrl, int64_t limit, hipStream_t st);
 hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st);
-// fused-norm filter (knn_fused.hip): rows augmented to d + 16 bf16 (k_aug_rows), d in {64, 128, 256}
+// fused-norm filter (knn_fused.hip), d in {64, 128, 256}: train as tile blocks [bn rows rn(t) |
+// bn fp32 norms | tile statistics] (k_tn_rows), each accumulator starting from the norms
 bool knn_fused_supported(int d);
 FilterPlan knn_fused_plan(int d, int k);  // nw == 0: k too large
 hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu);
@@ -158,7 +160,8 @@ hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu);
 // a.seg_len / nseg instead: the segment schedule, n_qtiles * nseg blocks.)
 int knn_fused_schedule(GemmFilterArgs& a, int slots, int* nseg);
 hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st);
-// x [n_valid][ld] (fp32 or bf16) -> bf16 [n][d + 16]: rn(scale * x) | split of norms[r] (or 1 1 1) | 0,
+// (study build KNN_STUDY_AUG64 only, d = 64) x [n_valid][ld] (fp32 or bf16) -> bf16 [n][d + 16]:
+// rn(scale * x) | split of norms[r] (or 1 1 1) | 0,
 // and (tstat != NULL, train) the 64-row tile statistics in columns d+8..d+10 of rows 32i;
 // rows n_valid .. n-1 (train: padding to the 64-row tile grid) never pass the filter
 hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int64_t n_valid, int ld, int d, const float* norms,
@@ -169,7 +172,7 @@ hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int64_t n_val
 hipError_t knn_launch_tn_rows(const void* x, int elem, int64_t n, int64_t n_valid, int ld, int d, const float* norms,
                               float scale, void* out, const float4* tstat, int bn, hipStream_t st,
                               const int32_t* gate = nullptr);
-// bytes per operand row of the fused filter's tile image (2d + 32 with the augmented block, or 2d)
+// bytes per operand row of the fused filter's tile image: 2d (2d + 32 in the KNN_STUDY_AUG64 build)
 int knn_fused_row_bytes(int d);
 hipError_t knn_launch_merge(const MergeArgs& a, hipStream_t st);
 hipError_t knn_launch_generate(const GenerateArgs& a, hipStream_t st);

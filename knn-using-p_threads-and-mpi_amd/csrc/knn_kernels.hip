@@ -1380,7 +1380,10 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
 // One wave per query merges the nsrc*k keys with the same wave list, so ties keep the
 // lower GLOBAL index exactly like the reference's serial scan over the whole train set,
 // then votes over the k winners: a shard's winners are a prefix of its list, found by
-// key <= the k-th key.  LDS per wave: counts [C] i32.
+// key <= the k-th key.  LDS per wave: counts [C] i32.  A source list must ascend by (dist,
+// idx) (the merge reads it in sorted runs and stops at the first batch that cannot pass):
+// every batch it reads is checked (adjacent lanes, and its first key against the previous
+// batch's last) and a descent sets KNN_STATUS_UNSORTED (knn_merge_vote_device: KNN_EINVAL).
 // ---------------------------------------------------------------------------------
 template <int R>
 __global__ __launch_bounds__(256) void k_merge_vote(MergeArgs a) {
@@ -1398,14 +1401,25 @@ __global__ __launch_bounds__(256) void k_merge_vote(MergeArgs a) {
 #pragma unroll
     for (int r = 0; r < R; r++) T[r] = KEY_NONE;
     u64 kth = KEY_NONE;
+    bool unsorted = false;
     for (int s = 0; s < a.nsrc; s++) {
         const int32_t* rec = a.rec + ((int64_t)s * a.nq + q) * 3 * k;
+        u64 last = 0;  // the previous batch's last key
         for (int e0 = 0; e0 < k; e0 += 64) {
             const int e = e0 + lane;
             u64 key = KEY_NONE;
             if (e < k) {
                 const int32_t ix = rec[k + e];
                 if (ix >= 0) key = make_key(__int_as_float(rec[e]), (uint32_t)ix);
+            }
+            {
+                const int pl = lane == 0 ? 0 : lane - 1;
+                const u64 prev = lane == 0 ? last
+                                           : (((u64)(uint32_t)__shfl((int)(uint32_t)(key >> 32), pl) << 32) |
+                                              (u64)(uint32_t)__shfl((int)(uint32_t)key, pl));
+                if (__ballot(key < prev)) unsorted = true;
+                last = (((u64)(uint32_t)__shfl((int)(uint32_t)(key >> 32), 63) << 32) |
+                        (u64)(uint32_t)__shfl((int)(uint32_t)key, 63));
             }
             // a source list ascends by key (a shard's exact top-k, or a segment's), so a batch
             // is a sorted run: passing keys are its prefix, none past the first that fails
@@ -1415,6 +1429,7 @@ __global__ __launch_bounds__(256) void k_merge_vote(MergeArgs a) {
             kth = list_at(T, k - 1);
         }
     }
+    if (unsorted && lane == 0) atomicOr(a.status, KNN_STATUS_UNSORTED);
     if (a.labels) {
         // segments of one train set (k_direct_tile): indices are local rows of a.labels
         finish_query<R>(T, k, a.C, a.labels, lds_counts ? counts : nullptr, q, a.out, a.status);

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Same-box A/B studies of the filter kernel: a library whose knn_fused.hip comes from a git
+# revision (or the working tree, "."), compiled with extra flags, linked with the current
+# objects of everything else.  Select it with KNN_AMD_LIB=<path> (the package's loader).
+#   bash scripts/build_variant.sh base HEAD              -> build/study/libknn_amd_base.so
+#   bash scripts/build_variant.sh stamps . -DKNN_STUDY_STAMPS
+set -e
+NAME=$1; REV=$2; shift 2
+P=$(cd "$(dirname "$0")/../knn-using-p_threads-and-mpi_amd" && pwd)
+cd "$P"
+make -s libknn_amd.so
+mkdir -p build/study
+SRC=csrc/.variant_${NAME}.hip
+if [ "$REV" = "." ]; then cp csrc/knn_fused.hip $SRC; else git show "$REV:knn-using-p_threads-and-mpi_amd/csrc/knn_fused.hip" > $SRC; fi
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" -c -o build/study/knn_fused_$NAME.o $SRC
+rm -f $SRC
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/study/libknn_amd_$NAME.so build/knn_kernels.o \
+    build/study/knn_fused_$NAME.o build/knn_capi.o build/knn_comm.o build/knn_arff.o build/knn_build_id.o -ldl
+echo "built build/study/libknn_amd_$NAME.so"

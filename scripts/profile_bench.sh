@@ -3,7 +3,8 @@
 #   1. rocprofv3 --kernel-trace --stats           -> per-kernel average durations
 #   2. rocprofv3 --pmc FETCH_SIZE                 -> HBM read bytes   (own pass)
 #   3. rocprofv3 --pmc WRITE_SIZE                 -> HBM write bytes  (own pass)
-#   4. rocprofv3 --pmc SQ_* / GRBM_GUI_ACTIVE     -> MFMA busy, clock (own pass)
+#   4. rocprofv3 --pmc SQ_* / GRBM_GUI_ACTIVE     -> MFMA busy, waits, clock (own pass)
+#   5. rocprofv3 --pmc SQ_*LDS* ...               -> LDS instructions, array-busy cycles (own pass)
 # Outputs land in gpurun_out/prof_*; scripts/summarize_profile.py turns them into
 # profiles/<tag>_*.{csv,json}.  Every pass runs under its own time limit and the chain
 # stops at the first failure.
@@ -24,7 +25,12 @@ echo "fetch pass ok"
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/${PT}_write -o run \
     -- python3 $BENCH > $OUT/${PT}_write.log 2>&1 || { echo "write pass failed"; exit 1; }
 echo "write pass ok"
-timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
+timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
     --output-format csv -d $OUT/${PT}_sq -o run \
     -- python3 $BENCH > $OUT/${PT}_sq.log 2>&1 || { echo "sq pass failed"; exit 1; }
 echo "sq pass ok"
+# LDS / instruction-mix pass (the filter's LDS load: reads per MFMA, array-busy cycles, waits)
+timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE \
+    --output-format csv -d $OUT/${PT}_lds -o run \
+    -- python3 $BENCH > $OUT/${PT}_lds.log 2>&1 || { echo "lds pass failed"; exit 1; }
+echo "lds pass ok"

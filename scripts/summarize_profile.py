@@ -34,7 +34,7 @@ def main():
             dur[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
     counters = defaultdict(lambda: defaultdict(list))
     rows_out = []
-    for p in (pt + "_fetch", pt + "_write", pt + "_sq"):
+    for p in (pt + "_fetch", pt + "_write", pt + "_sq", pt + "_lds"):
         path = os.path.join(src, p, "run_counter_collection.csv")
         if not os.path.exists(path):
             continue
@@ -54,8 +54,16 @@ def main():
     def mean(xs):
         return sum(xs) / len(xs) if xs else None
 
-    # the bench workload these counters were taken on (bench.py pmc_traffic(config))
-    out = {"tag": tag, "config": sys.argv[3] if len(sys.argv) > 3 else "A"}
+    # the bench workload these counters were taken on: bench.py's own key (pmc_key), from the
+    # JSON line of the trace pass; argv[3] only when that line is missing
+    key = sys.argv[3] if len(sys.argv) > 3 else "A"
+    try:
+        with open(os.path.join(src, pt + "_trace.log")) as f:
+            line = [l for l in f.read().splitlines() if l.startswith("{")][-1]
+        key = json.loads(line).get("pmc_key", key)
+    except (OSError, IndexError, ValueError):
+        pass
+    out = {"tag": tag, "config": key}
     # the filter launch that did the work: the matching kernel with the longest trace time
     # (AUTO's gated re-run launches the split filter, which exits at once)
     cands = [k for k in counters if "k_gemm_filter" in k or "k_gemm_fused" in k]
@@ -66,6 +74,9 @@ def main():
         write = mean([v for v, _ in c.get("WRITE_SIZE", [])])
         gui = c.get("GRBM_GUI_ACTIVE", [])
         busy = mean([v for v, _ in c.get("SQ_VALU_MFMA_BUSY_CYCLES", [])])
+        # quad-cycle counters (MI355X_MICROARCH.md): fractions of SQ_WAVE_CYCLES
+        wave = mean([v for v, _ in c.get("SQ_WAVE_CYCLES", [])])
+        waits = {n: mean([v for v, _ in c.get(n, [])]) for n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")}
         mfma = mean([v for v, _ in c.get("SQ_INSTS_MFMA", [])])
         valu = mean([v for v, _ in c.get("SQ_INSTS_VALU", [])])
         clk = mean([v / 8.0 / w for v, w in gui]) if gui else None
@@ -85,8 +96,29 @@ def main():
             "mfma_busy_frac": busy / (simds * clk * wall) if busy and clk and wall else None,
             "trace_avg_ms": 1e3 * mean(dur.get(k, [])) if dur.get(k) else None,
         })
+        for n, v in waits.items():
+            if v is not None and wave:
+                out[n.lower() + "_frac"] = v / wave
+        # every counter of the filter launch, averaged over its launches
+        out["counters"] = {n: mean([v for v, _ in vals]) for n, vals in sorted(c.items())}
     with open(os.path.join(prof, f"{tag}_pmc_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
+    # the index bench.py reads (pmc_traffic): the newest summary per workload key (a study
+    # build's profile, KNN_PMC_NO_INDEX=1, stays out of it)
+    if os.environ.get("KNN_PMC_NO_INDEX") == "1":
+        print(json.dumps(out, indent=1))
+        return
+    idx_path = os.path.join(prof, "pmc_latest.json")
+    try:
+        with open(idx_path) as f:
+            idx = json.load(f)
+    except (OSError, ValueError):
+        idx = {}
+    idx[key] = {"tag": tag, "file": f"profiles/{tag}_pmc_traffic.json",
+                "gemm_filter_bytes_per_launch": out.get("gemm_filter_bytes_per_launch"),
+                "trace_avg_ms": out.get("trace_avg_ms"), "kernel": out.get("kernel")}
+    with open(idx_path, "w") as f:
+        json.dump(idx, f, indent=1, sort_keys=True)
     print(json.dumps(out, indent=1))
 
 
