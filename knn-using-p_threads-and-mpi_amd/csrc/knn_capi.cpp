@@ -64,6 +64,7 @@ struct knn_ctx {
     DBuf seg_rec;           // k_direct_tile segment records [nseg][nq][3][k]
     DBuf tmax;              // fused filter: per-64-row train stats {max tn, max |t - rt|, max |rt|, 0}
     DBuf cursor;            // fused filter: per-XCD scan cursors (64-row units; performance hint only)
+    DBuf lshare;            // fused filter: per (query, piece) threshold lists shared between pieces
     DBuf qstat;             // fused filter: per-query {|q|, |q - rq|} upper bounds
     DBuf tblk;              // fused filter: train tile blocks [bn rows rn(t) | bn norms | tile stats]
     DBuf tctrl;             // the train norms' share of the status word: [unsafe bits, 0, max norm, 0]
@@ -369,7 +370,7 @@ int max_splits(int64_t nt, int k, int cap) {
 }
 
 int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int rb, int k, int cap,
-                  bool fused = false, int d = 0) {
+                  bool fused = false, int d = 0, int64_t nq = 0) {
     if (c->train_splits > 0) return std::min(8, c->train_splits);
     // More segments shrink the partial last wave of blocks (measured on config A:
     // S=3 224 ms, S=5 217 ms, S=8 216 ms), but each segment must fit its rows in its
@@ -378,7 +379,7 @@ int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int
     // tile; the slice gets a 1.5x margin.  Overflowing queries still finish exactly,
     // on the slow full-scan fallback.
     int occ = 1;
-    const hipError_t oe = fused ? knn_fused_occupancy(d, k, &occ) : knn_gemm_filter_occupancy(dtype, rb, k, &occ);
+    const hipError_t oe = fused ? knn_fused_occupancy(d, k, &occ, nq, c->num_cus) : knn_gemm_filter_occupancy(dtype, rb, k, &occ);
     if (oe != hipSuccess || occ < 1) occ = 1;
     const int64_t slots = (int64_t)occ * c->num_cus;
     int best = 1;
@@ -420,7 +421,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
 
     // bf16 MFMA operands (rounded fp32 rows or bf16 data) run the fused-norm filter
     const bool fused = (felem == ELEM_ROUND || felem == ELEM_BF16) && knn_fused_supported(d) &&
-                       knn_fused_plan(d, k).nw > 0;
+                       knn_fused_plan(d, k, nq, c->num_cus).nw > 0;
     float coef, eta;
     if (fused) {
         certificate_fused(d, felem == ELEM_ROUND, &coef, &eta);
@@ -434,7 +435,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     // context caches train (no train pass at all then; main.cpp:40-43 re-reads every train row
     // per query, this is the part of that work that depends on train alone)
     const bool fused_tn = fused && knn_fused_row_bytes(d) == 2 * d;
-    const int bn_f = fused ? 32 * knn_fused_plan(d, k).rg : 0;
+    const int bn_f = fused ? 32 * knn_fused_plan(d, k, nq, c->num_cus).rg : 0;
     const bool own_train = tr->feat == c->h_train.p;  // knn_predict's uploaded copy
     auto& tp = c->tprep;
     const bool prep_hit = fused_tn && !gate && c->cache_train && tp.valid && tp.feat == tr->feat && tp.n == nt &&
@@ -554,7 +555,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         ftrain = c->pad_t.p;
     }
 
-    const FilterPlan plan = fused ? knn_fused_plan(d, k) : knn_gemm_filter_plan(kelem, rb, k);
+    const FilterPlan plan = fused ? knn_fused_plan(d, k, nq, c->num_cus) : knn_gemm_filter_plan(kelem, rb, k);
     const int64_t n_qtiles = (nq + plan.bm - 1) / plan.bm;
     GemmFilterArgs g{};
     g.nt = nt; g.n_qtiles = (int)n_qtiles;
@@ -563,13 +564,13 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     int nseg = 0;
     if (fused && c->train_splits <= 0) {
         int occ = 1;
-        if (knn_fused_occupancy(d, k, &occ) != hipSuccess || occ < 1) occ = 1;
+        if (knn_fused_occupancy(d, k, &occ, nq, c->num_cus) != hipSuccess || occ < 1) occ = 1;
         int nb = 1;
         knn_fused_schedule(g, occ * c->num_cus, &nb);
         if (nb <= max_splits(nt, k, cap)) nseg = nb;
     }
     if (nseg == 0) {
-        nseg = choose_splits(c, n_qtiles, nt, kelem, rb, k, cap, fused, d);
+        nseg = choose_splits(c, n_qtiles, nt, kelem, rb, k, cap, fused, d, nq);
         g.g2 = -1;  // segment schedule
     }
     int64_t seg_len = (nt + nseg - 1) / nseg;
@@ -592,12 +593,22 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         HIP_OR_FAIL(c, hipMemsetAsync(c->cursor.p, 0, sizeof(uint32_t) * 8, st));
         g.cursor = c->cursor.as<uint32_t>();
     }
+    // the pieces of a query share their threshold lists, not just their k-th values: the
+    // union's k-th smallest U is the bound a single scan would have (KNN_NO_LIST_SHARE=1: off)
+    static const bool no_lshare = getenv("KNN_NO_LIST_SHARE") != nullptr;
+    if (fused && !no_lshare && plan.kr > 0 && nseg > 1) {
+        g.lshare_w = plan.kr == 32 ? 32 : 16;
+        const int64_t nls = nq * (int64_t)nseg * g.lshare_w;
+        HIP_OR_FAIL(c, c->lshare.ensure(sizeof(float) * nls));
+        HIP_OR_FAIL(c, knn_launch_fill_u32(c->lshare.as<uint32_t>(), nls, 0x7f800000u, gate, st));  // +inf
+        g.lshare = c->lshare.as<float>();
+    }
     g.status = c->ctrl.as<int32_t>();
     g.gate = gate;
     if (fused && g.g2 >= 0 && nseg > 1)  // whole query tiles write only sub-slice 0
         HIP_OR_FAIL(c, hipMemsetAsync(c->cnt.p, 0, sizeof(int32_t) * 2 * nseg * nq, st));
     stage_begin(c, st, gate ? "gemm_filter_rerun" : "gemm_filter");
-    if (fused) HIP_OR_FAIL(c, knn_launch_fused(g, st));
+    if (fused) HIP_OR_FAIL(c, knn_launch_fused(g, plan, st));
     else HIP_OR_FAIL(c, knn_launch_gemm_filter(g, kelem, rb, st));
     stage_end(c, st);
 
@@ -696,7 +707,7 @@ void knn_destroy(knn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (DBuf* b : {&c->tnorm, &c->tnp, &c->qnorm, &c->gthr, &c->cnt, &c->cand,
-                    &c->fb_list, &c->ctrl, &c->scratch, &c->split_t, &c->split_q, &c->pad_t, &c->seg_rec, &c->tmax, &c->qstat, &c->tblk, &c->tctrl, &c->cursor, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
+                    &c->fb_list, &c->ctrl, &c->scratch, &c->split_t, &c->split_q, &c->pad_t, &c->seg_rec, &c->tmax, &c->qstat, &c->tblk, &c->tctrl, &c->cursor, &c->lshare, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
                     &c->h_dist, &c->h_idx})
         b->release();
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "knn_device.h"
 #include "knn_kernels.h"
@@ -31,6 +32,9 @@ static constexpr int FUSED_PF = KNN_STUDY_PF;  // (study builds pf4 / pf8)
 static constexpr int FUSED_DEFER_EVERY = 64;  // 8-wave heap shapes: tiles between flushes of the queued values
 static constexpr int FUSED_SHARE_EVERY = 64;  // tiles between threshold exchanges of a query's pieces (gthr)
 static constexpr int FUSED_RQ = 4;            // queued passing values per lane (heap shapes)
+#ifndef KNN_FUSED_LIST_SHARE
+#define KNN_FUSED_LIST_SHARE 0                // pieces exchange threshold lists (a.lshare)
+#endif
 
 // ---------------------------------------------------------------------------------
 // k_aug_rows<E>: rows of the fused filter, [n][d + 16] bf16.  Element c < d is
@@ -210,7 +214,7 @@ extern "C" int knn_debug_stamps(unsigned long long* out, int reset) {
 }
 #endif
 
-template <int RB, int NBUF, int NW, int RG, int KR>
+template <int RB, int NBUF, int NW, int QG, int RG, int KR>
 __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int qt, const int seg,
                                             const int64_t row_begin, const int64_t row_end) {
     // TN (RB = 2d, the product): train tiles carry their rows' norms in a header, and each
@@ -220,8 +224,11 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     constexpr bool TN = RB % 64 == 0;
     constexpr int BN_ = 32 * RG;
     constexpr int HS = TN ? BN_ / 4 + 1 : 0;  // header slots: BN fp32 norms + the statistics
-    typedef FilterTile<RB, NW, 1, RG, HS> FT;
-    constexpr int NACC = RG, BN = FT::BN, BM = FT::BM, STRIDE = FT::STRIDE, SLOTS = FT::SLOTS;
+    // QG 32-query groups per wave (QG = 2: 64 queries per wave on 32-row tiles, the register-list
+    // shapes only): accumulator c holds row group c % RG against query group c / RG, so each A
+    // fragment read from LDS feeds QG MFMAs and each tile copy serves 32 QG NW queries
+    typedef FilterTile<RB, NW, QG, RG, HS> FT;
+    constexpr int NACC = FT::NACC, BN = FT::BN, BM = FT::BM, STRIDE = FT::STRIDE, SLOTS = FT::SLOTS;
     constexpr int DMA_INS = FT::DMA_INS, TILE = FT::TILE, HDR = FT::HDR;
     // bytes of one tile in the train operand (TN: a block of rows + header; else rows of pitch RB)
     constexpr int64_t TB = (int64_t)BN * RB + 16 * HS;
@@ -229,17 +236,19 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     constexpr int DMA_PER_WAVE = (DMA_INS + NW - 1) / NW;
     constexpr int NS = RB / 32;                  // k-steps: d/16 feature steps (+ the norm step)
     constexpr int VPS = (16 + NS - 1) / NS;      // fast-test values per k-step per accumulator
-    static_assert(NBUF == 2 || NBUF == 4, "tile buffers: two, or four (tiles in pairs)");
+    static_assert(NBUF == 2 || NBUF == 4 || NBUF == 8, "tile buffers: two, four (tiles in pairs) or eight (quads)");
     // NBUF = 4: tiles go in pairs -- one barrier per pair; the DMA of tile it + 2 is issued
     // during step it into the buffer tile it - 2 used (read before this pair's barrier)
     // (quads -- eight buffers, one barrier per four tiles -- and six-buffer pairs with the DMA
     // two pairs ahead and counted vmcnt waits measured no faster: DESIGN.md, round-3 studies)
-    constexpr int GRP = NBUF == 4 ? 2 : 1;
+    constexpr int GRP = NBUF >= 4 ? NBUF / 2 : 1;  // tiles per barrier
     constexpr bool PAIR = GRP > 1;
     constexpr int AHEAD = PAIR ? GRP : NBUF - 1;  // tiles between a step and the tile it DMAs
     static_assert(RG == 1 || RG == 2, "row groups");
     static_assert(KR == 0 || KR == 16 || KR == 32, "register lists: k <= 16, k <= 32, or LDS heaps");
     constexpr bool RL = KR > 0;                   // thresholds from per-lane register lists (else LDS heaps)
+    // (QG = 2 on 64-row tiles, four accumulators, was tried at d = 64: 1.5 KB of scratch spills)
+    static_assert(QG == 1 || (QG == 2 && RG == 1 && RL), "64-query waves: 32-row tiles, register lists");
     constexpr bool HALVES = KR == 32;             // one list per lane half (below): k <= 2 LL
     constexpr int LL = 16;                        // register list length
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -265,58 +274,77 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         }
     }
 
-    // this lane's query (both lane halves hold the same query, different rows)
-    const int jl = wave * 32 + j;
-    const int64_t q = (int64_t)qt * BM + jl;
-    const bool qvalid = q < a.nq;
-    uint4 qf[NS];
-    {
+    // this lane's queries, one per query group g (both lane halves hold the same queries,
+    // different rows): query jl[g] of the block
+    int jl[QG];
+    int64_t q[QG];
+    bool qvalid[QG];
+    uint4 qf[QG][NS];
+    float qn[QG], thr[QG], published[QG];
+    int ccnt[QG];  // candidates this lane half kept, per query
+#pragma unroll
+    for (int g = 0; g < QG; g++) {
+        jl[g] = (wave * QG + g) * 32 + j;
+        q[g] = (int64_t)qt * BM + jl[g];
+        qvalid[g] = q[g] < a.nq;
         const unsigned char* qrow = reinterpret_cast<const unsigned char*>(a.test) +
-                                    (qvalid ? q : 0) * (int64_t)a.ld_q * 2;
+                                    (qvalid[g] ? q[g] : 0) * (int64_t)a.ld_q * 2;
 #pragma unroll
         for (int s = 0; s < NS; s++)
-            qf[s] = qvalid ? *reinterpret_cast<const uint4*>(qrow + 32 * s + 16 * h) : make_uint4(0u, 0u, 0u, 0u);
+            qf[g][s] = qvalid[g] ? *reinterpret_cast<const uint4*>(qrow + 32 * s + 16 * h)
+                                 : make_uint4(0u, 0u, 0u, 0u);
+        qn[g] = qvalid[g] ? a.qnorm[q[g]] : 0.0f;
+        thr[g] = qvalid[g] ? o2f(a.gthr[q[g]]) : -INF;
+        published[g] = thr[g];
+        ccnt[g] = 0;
     }
-    const float qn = qvalid ? a.qnorm[q] : 0.0f;
-    float thr = qvalid ? o2f(a.gthr[q]) : -INF;
-    float published = thr;
-    float root = INF;  // this query's heap root, mirrored in both lanes
-    int ccnt = 0;      // candidates this lane half kept
-    float tfb;         // tf without the tile term
-    auto make_tfb = [&]() __attribute__((always_inline)) {
-        tfb = qvalid ? ((thr - qn) + fmaf(coef, qn, eta)) + 0x1p-18f * (fabsf(thr) + qn) : -INF;
+    float root = INF;  // (heap shapes, QG = 1) this query's heap root, mirrored in both lanes
+    float tfb[QG];     // tf without the tile term
+    auto make_tfb = [&](int g) __attribute__((always_inline)) {
+        tfb[g] = qvalid[g] ? ((thr[g] - qn[g]) + fmaf(coef, qn[g], eta)) + 0x1p-18f * (fabsf(thr[g]) + qn[g]) : -INF;
     };
-    make_tfb();
+#pragma unroll
+    for (int g = 0; g < QG; g++) make_tfb(g);
     // tile term: tq = {the tile's maximum norm tmax, the operand-rounding bound of this query
     // against the tile's rows, 2 (|q| max|t - rt| + |q - rq| max|rt|) (1 + 2^-17)}
-    auto tf_of = [&](float2 tq) __attribute__((always_inline)) { return fmaf(coef + 0x1p-18f, tq.x, tfb) + tq.y; };
-    float qe2 = 0.0f, eq2 = 0.0f;  // 2 |q| and 2 |q - rq|, rounded up
-    if (qvalid) {
-        const float2 qs = a.qstat[q];
-        qe2 = 2.0f * qs.x * (1.0f + 0x1p-17f);
-        eq2 = 2.0f * qs.y * (1.0f + 0x1p-17f);
+    auto tf_of = [&](int g, float2 tq) __attribute__((always_inline)) {
+        return fmaf(coef + 0x1p-18f, tq.x, tfb[g]) + tq.y;
+    };
+    float qe2[QG], eq2[QG];  // 2 |q| and 2 |q - rq|, rounded up
+#pragma unroll
+    for (int g = 0; g < QG; g++) {
+        qe2[g] = eq2[g] = 0.0f;
+        if (qvalid[g]) {
+            const float2 qs = a.qstat[q[g]];
+            qe2[g] = 2.0f * qs.x * (1.0f + 0x1p-17f);
+            eq2[g] = 2.0f * qs.y * (1.0f + 0x1p-17f);
+        }
     }
-    // the tile's statistics, from row 0 of its LDS image (augmented columns d+8..d+10, see
-    // k_aug_rows): one broadcast ds_read_b64, in order with the fragment reads -- no scalar
-    // memory load in the loop
-    // (TN: the header's last slot, fp32)
-    auto tile_q = [&](int buf) __attribute__((always_inline)) -> float2 {
+    // the tile's statistics, from its LDS image (TN: the header's last slot, fp32; the
+    // KNN_STUDY_AUG64 layout: augmented columns d+8..d+10 of row 0, bf16): one broadcast read,
+    // in order with the fragment reads -- no scalar memory load in the loop
+    struct TQ { float2 v[QG]; };
+    auto tile_q = [&](int buf) __attribute__((always_inline)) -> TQ {
+        float tx, ty, tz;
         if constexpr (TN) {
             const float4 w = *reinterpret_cast<const float4*>(tiles + buf * TILE + HDR + 4 * BN);
-            return make_float2(w.x, fmaf(qe2, w.y, eq2 * w.z));
+            tx = w.x; ty = w.y; tz = w.z;
         } else {
             const uint2 w = *reinterpret_cast<const uint2*>(tiles + buf * TILE + (RB - 16));
-            const float tx = __uint_as_float(w.x << 16), ty = __uint_as_float(w.x & 0xffff0000u);
-            const float tz = __uint_as_float(w.y << 16);
-            return make_float2(tx, fmaf(qe2, ty, eq2 * tz));
+            tx = __uint_as_float(w.x << 16); ty = __uint_as_float(w.x & 0xffff0000u);
+            tz = __uint_as_float(w.y << 16);
         }
+        TQ r;
+#pragma unroll
+        for (int g = 0; g < QG; g++) r.v[g] = make_float2(tx, fmaf(qe2[g], ty, eq2[g] * tz));
+        return r;
     };
 
     // tiles of the piece, rounded up to an even count: the scan loop below runs tiles in twos
     // with no exit between them, so only accB is live out of it (with an odd tail the compiler
     // copies both accumulator sets -- 32 v_mov -- at every back edge).  The extra tile reads the
-    // next 64 rows (another piece's, or the padding the augmented train rows carry past the
-    // tile grid, run_gemm), which the row_end test rejects.
+    // next BN rows (another piece's, or the padding the train tile blocks carry past the
+    // 64-row grid, run_gemm), which the row_end test rejects.
     const int ntiles = (row_end > row_begin) ? ((int)((row_end - row_begin + BN - 1) / BN) + 1) & ~1 : 0;
     // Scan order (a.cursor set: the host does so for the multi-segment schedule): the piece's
     // tiles rotated to start where this XCD's other blocks are (per XCD: the 64-row unit the last
@@ -348,7 +376,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
 
     // ---- LDS-DMA of tiles (same image as k_gemm_filter: slot P -> row P / SLOTS, slot P % SLOTS,
     // the pad slot duplicates slot 0; rows past row_end are read (padding or the next piece's
-    // rows) and rejected by index).  Every tile is whole: the augmented train rows are padded to
+    // rows) and rejected by index).  Every tile is whole: the train tile blocks are padded to
     // the 64-row grid (run_gemm), so a piece is always the scalar tile base + this lane's fixed
     // offset -- no per-tile address arithmetic in VGPRs.
     // (piece ins = wave + NW i; rotating the DMA_INS % NW remainder pieces between even and odd
@@ -366,8 +394,8 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     }
     const uint32_t lds_tiles = __builtin_amdgcn_readfirstlane(lds_addr(tiles));
     struct DmaTile { const unsigned char* src; uint32_t lds; };
-    // the source of a tile: its block in the train operand (rows are whole 64-row tiles: the
-    // piece's first row and BN are multiples of 64)
+    // the source of a tile: its block in the train operand (the piece's first row is a multiple
+    // of 64, BN divides 64)
     const int64_t TBR = TN ? TB : (int64_t)BN * ldb;  // operand bytes per tile
     const unsigned char* piece_src = trainb + (row_begin / BN) * TBR;
     auto dma_desc = [&](int buf, int t) -> DmaTile {  // logical tile t of the piece
@@ -404,28 +432,31 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         }
     };
     auto step = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int buf, bool dma_on, const DmaTile& dd,
-                    float tf, bool pre) -> uint32_t {
+                    const float (&tf)[QG], bool pre) -> uint32_t {
         const unsigned char* tile = tiles + buf * TILE;
         const unsigned char* a0p = tile + j * STRIDE + 16 * h;
         const unsigned char* a1p = tile + ((RG == 2 ? 32 : 0) + j) * STRIDE + 16 * h;
+        // each accumulator's chain starts from its rows' norms: register r of row group rg is row
+        // 32 rg + (r & 3) + 8 (r >> 2) + 4h (four broadcast ds_read_b128 per row group; the QG
+        // accumulators of a row group share them as the first MFMA's C operand)
+        // (the norms land in row group rg's query-group-0 accumulator X[rg]; at k-step 0 the other
+        // query groups' MFMAs take them as their C operand first, then X[rg]'s own -- no copy)
         if constexpr (TN) {
-            // register r of accumulator c is row 32c + (r & 3) + 8 (r >> 2) + 4h: its norm starts
-            // the chain (four broadcast ds_read_b128 per accumulator)
             const unsigned char* hn = tile + HDR + 4 * (4 * h);
 #pragma unroll
-            for (int c = 0; c < NACC; c++) {
+            for (int rg = 0; rg < RG; rg++) {
 #pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const float4 v = *reinterpret_cast<const float4*>(hn + 4 * (32 * c + 8 * g));
-                    X[c][4 * g] = v.x;
-                    X[c][4 * g + 1] = v.y;
-                    X[c][4 * g + 2] = v.z;
-                    X[c][4 * g + 3] = v.w;
+                for (int g4 = 0; g4 < 4; g4++) {
+                    const float4 v = *reinterpret_cast<const float4*>(hn + 4 * (32 * rg + 8 * g4));
+                    X[rg][4 * g4] = v.x;
+                    X[rg][4 * g4 + 1] = v.y;
+                    X[rg][4 * g4 + 2] = v.z;
+                    X[rg][4 * g4 + 3] = v.w;
                 }
             }
         } else {
 #pragma unroll
-            for (int c = 0; c < NACC; c++) X[c] = floatx16{};
+            for (int rg = 0; rg < RG; rg++) X[rg] = floatx16{};
         }
         float mn[NACC];
 #pragma unroll
@@ -449,9 +480,12 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                 if (RG == 2) xb[s + PF] = *reinterpret_cast<const uint4*>(a1p + 32 * (s + PF));
             }
 #pragma unroll
-            for (int c = 0; c < NACC; c++) {
-                const bf16x8 A = __builtin_bit_cast(bf16x8, (RG == 2 && c) ? xb[s] : xa[s]);
-                X[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, __builtin_bit_cast(bf16x8, qf[s]), X[c], 0, 0, 0);
+            for (int cc = 0; cc < NACC; cc++) {
+                const int c = s == 0 ? NACC - 1 - cc : cc;  // (k-step 0: query group 0 last)
+                const int rg = c % RG, g = c / RG;
+                const bf16x8 A = __builtin_bit_cast(bf16x8, (RG == 2 && rg) ? xb[s] : xa[s]);
+                X[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, __builtin_bit_cast(bf16x8, qf[g][s]),
+                                                               s == 0 ? X[rg] : X[c], 0, 0, 0);
                 if (!KNN_STUDY_NO_EPI) {
 #pragma unroll
                     for (int v = s * VPS; v < (s + 1) * VPS && v < 16; v++) mn[c] = fminf(mn[c], Y[c][v]);
@@ -467,29 +501,29 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         // (pass_set) -- usually one of the two
         uint32_t u = 0u;
 #pragma unroll
-        for (int c = 0; c < NACC; c++) u |= __ballot(mn[c] <= tf) != 0ull ? (0xffffu << (16 * c)) : 0u;
+        for (int c = 0; c < NACC; c++) u |= __ballot(mn[c] <= tf[c / RG]) != 0ull ? (0xffffu << (16 * c)) : 0u;
         return u;
     };
 
-    // append candidate (L, U) of global row t to this lane half's sub-slice (past its
-    // capacity: counted only, the rescore then sends the query to the exact scan)
-    auto store_cand = [&](float L, float U, int64_t t) __attribute__((always_inline)) {
-        if (ccnt < cap_sub) {
-            const int64_t o = q * (int64_t)a.cap + (int64_t)(2 * seg + h) * cap_sub + ccnt;
+    // append candidate (L, U) of global row t to query group g's sub-slice of this lane half
+    // (past its capacity: counted only, the rescore then sends the query to the exact scan)
+    auto store_cand = [&](int g, float L, float U, int64_t t) __attribute__((always_inline)) {
+        if (ccnt[g] < cap_sub) {
+            const int64_t o = q[g] * (int64_t)a.cap + (int64_t)(2 * seg + h) * cap_sub + ccnt[g];
             a.cand[o] = CandRec{(int32_t)t, L, U};
         }
-        ccnt++;
+        ccnt[g]++;
     };
-    // keep candidate (L, U) of global row t: the exact test against the current threshold,
-    // the candidate store into this lane half's sub-slice, and, if U beats the heap root, a
-    // sift-down of the query's 4-ary max-heap (node n >= 1 in H[n-1], the root in H[hs-1]:
-    // the four children of node i are one aligned 16-byte read at H[4i]).  Only one lane of
-    // a query runs it at a time.
+    // (heap shapes, QG = 1) keep candidate (L, U) of global row t: the exact test against the
+    // current threshold, the candidate store into this lane half's sub-slice, and, if U beats
+    // the heap root, a sift-down of the query's 4-ary max-heap (node n >= 1 in H[n-1], the root
+    // in H[hs-1]: the four children of node i are one aligned 16-byte read at H[4i]).  Only one
+    // lane of a query runs it at a time.
     auto accept = [&](float L, float U, int64_t t) __attribute__((always_inline)) {
-        if (!(L <= thr)) return;
-        store_cand(L, U, t);
+        if (!(L <= thr[0])) return;
+        store_cand(0, L, U, t);
         if (U < root) {
-            float* H = topU + jl * hs;
+            float* H = topU + jl[0] * hs;
             int i = 0;
             float newroot = U;
             for (;;) {
@@ -504,7 +538,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             }
             H[i == 0 ? hs - 1 : i - 1] = U;
             root = newroot;
-            thr = fminf(thr, root);
+            thr[0] = fminf(thr[0], root);
         }
     };
     auto sync_roots = [&](int hh) __attribute__((always_inline)) {
@@ -513,22 +547,22 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
     };
-    auto publish = [&]() __attribute__((always_inline)) {
-        if (qvalid) {
-            thr = fminf(thr, root);
-            if (a.nseg > 1 && h == 0 && thr < published) {
-                atomicMin(&a.gthr[q], f2o(thr));
-                published = thr;
+    auto publish = [&]() __attribute__((always_inline)) {  // (heap shapes)
+        if (qvalid[0]) {
+            thr[0] = fminf(thr[0], root);
+            if (a.nseg > 1 && h == 0 && thr[0] < published[0]) {
+                atomicMin(&a.gthr[q[0]], f2o(thr[0]));
+                published[0] = thr[0];
             }
-            make_tfb();
+            make_tfb(0);
         }
     };
-    // certified bounds L <= D <= U of value y against tile stats tq: Delta = coef (qn + tmax)
-    // + eta + rho -- the tile's maximum norm tmax >= the row's norm, a slightly wider band
-    // (still L <= D <= U) for no per-value norm read
-    auto bounds = [&](float y, float2 tq, float& L, float& U) __attribute__((always_inline)) {
-        const float G = qn + y;
-        const float dl = fmaf(coef, qn + tq.x, eta) + tq.y;
+    // certified bounds L <= D <= U of value y of query group g against tile stats tq: Delta =
+    // coef (qn + tmax) + eta + rho -- the tile's maximum norm tmax >= the row's norm, a slightly
+    // wider band (still L <= D <= U) for no per-value norm read
+    auto bounds = [&](int g, float y, float2 tq, float& L, float& U) __attribute__((always_inline)) {
+        const float G = qn[g] + y;
+        const float dl = fmaf(coef, qn[g] + tq.x, eta) + tq.y;
         L = G - dl;
         U = G + dl;
     };
@@ -541,20 +575,20 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         if constexpr (NACC == 1) return Y[0][v & 15];
         else return (v >> 4) ? Y[1][v & 15] : Y[0][v & 15];
     };
-    // the values of Y some lane passes (bit 16c + r), for the accumulators set in acc: per
-    // group of 4 values (rows 8g .. 8g+3 of the lane half) one ballot of their minimum, then
-    // one v_cmp + ballot per value of the passing groups only
+    // (heap shapes) the values of Y some lane passes (bit 16c + r), for the accumulators set in
+    // acc: per group of 4 values (rows 8g .. 8g+3 of the lane half) one ballot of their minimum,
+    // then one v_cmp + ballot per value of the passing groups only
     auto pass_set = [&](floatx16 (&Y)[NACC], float tf, uint32_t acc) __attribute__((always_inline)) -> uint32_t {
         uint32_t u = 0u;
 #pragma unroll
         for (int c = 0; c < NACC; c++)
             if ((acc >> (16 * c)) & 1u) {  // (wave-uniform) only the accumulators that pass
 #pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const float gm = fminf(fminf(Y[c][4 * g], Y[c][4 * g + 1]), fminf(Y[c][4 * g + 2], Y[c][4 * g + 3]));
+                for (int g4 = 0; g4 < 4; g4++) {
+                    const float gm = fminf(fminf(Y[c][4 * g4], Y[c][4 * g4 + 1]), fminf(Y[c][4 * g4 + 2], Y[c][4 * g4 + 3]));
                     if (__ballot(gm <= tf)) {
 #pragma unroll
-                        for (int r = 4 * g; r < 4 * g + 4; r++)
+                        for (int r = 4 * g4; r < 4 * g4 + 4; r++)
                             u |= (__ballot(Y[c][r] <= tf) != 0ull ? 1u : 0u) << (16 * c + r);
                     }
                 }
@@ -579,7 +613,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                 if (!__ballot(p && h == hh)) continue;
                 if (p && h == hh && t < row_end) {
                     float L, U;
-                    bounds(y, tq, L, U);
+                    bounds(0, y, tq, L, U);
                     accept(L, U, t);
                 }
                 sync_roots(hh);
@@ -600,16 +634,19 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // v_med3); the bound is the larger of the two
     // halves' ceil(k/2)-th smallest -- at least 2 ceil(k/2) >= k kept rows have U <= it.  A
     // little looser than the exact k-th smallest, with no LDS heap and no turn-taking.
-    float lst[RL ? LL : 1];
+    // (QG = 2: one list per query group.)
+    float lst[QG][RL ? LL : 1];
     if constexpr (RL) {
         const int pads = LL - (HALVES ? (k + 1) / 2 : k);
 #pragma unroll
-        for (int i = 0; i < LL; i++) lst[i] = i < pads ? -INF : INF;
-    }
-    auto list_insert = [&](float w) __attribute__((always_inline)) {
+        for (int g = 0; g < QG; g++)
 #pragma unroll
-        for (int i = LL - 1; i >= 1; i--) lst[i] = __builtin_amdgcn_fmed3f(lst[i - 1], w, lst[i]);
-        lst[0] = fmin_fast(lst[0], w);
+            for (int i = 0; i < LL; i++) lst[g][i] = i < pads ? -INF : INF;
+    }
+    auto list_insert = [&](int g, float w) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = LL - 1; i >= 1; i--) lst[g][i] = __builtin_amdgcn_fmed3f(lst[g][i - 1], w, lst[g][i]);
+        lst[g][0] = fmin_fast(lst[g][0], w);
     };
     // the other lane half's copy of a word (v_permlane32_swap: one of the swap's two results
     // is this lane's own word, the other its partner's)
@@ -626,10 +663,11 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // unless the threshold is still loose).  Any processing order keeps every true neighbour:
     // a row is kept iff L <= the threshold at its turn, and the threshold is always the k-th
     // smallest U of kept rows.
-    auto lane_rounds = [&](floatx16 (&Y)[NACC], float tf, uint32_t u, auto&& fn) __attribute__((always_inline)) {
+    auto lane_rounds = [&](floatx16 (&Y)[NACC], const float (&tf)[QG], uint32_t u, auto&& fn) __attribute__((always_inline)) {
 #pragma unroll
         for (int c = 0; c < NACC; c++) {
             if (!((u >> (16 * c)) & 1u)) continue;  // (wave-uniform) no lane passes in c
+            const float tfc = tf[c / RG];
             // round 1: the highest passing index, its value, the lane's passing count
             // (a scan of the 16 values; scanning the highest passing group of four instead,
             // found by the group minima, measured 4-8 % slower overall: r03q)
@@ -639,7 +677,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             float yv = INF;
 #pragma unroll
             for (int r = 0; r < 16; r++) {
-                const bool p = Y[c][r] <= tf;
+                const bool p = Y[c][r] <= tfc;
                 idx = p ? r : idx;
                 yv = p ? Y[c][r] : yv;
                 cnt += p ? 1 : 0;
@@ -655,7 +693,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                     yv = INF;
 #pragma unroll
                     for (int r = 0; r < 16; r++) {
-                        const bool p = Y[c][r] <= tf && r < lim;
+                        const bool p = Y[c][r] <= tfc && r < lim;
                         idx = p ? r : idx;
                         yv = p ? Y[c][r] : yv;
                     }
@@ -666,34 +704,36 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             }
         }
     };
-    auto slow_rl = [&](floatx16 (&Y)[NACC], int tp, float tf, float2 tq, uint32_t u) {
+    auto slow_rl = [&](floatx16 (&Y)[NACC], int tp, const float (&tf)[QG], const TQ& tq, uint32_t u) {
         if constexpr (RL) {
             const int64_t tbase = tile_row(tp);
             auto visit = [&](int c, int idx, float yv) __attribute__((always_inline)) {
-                const int row = 32 * c + (idx & 3) + 8 * (idx >> 2) + 4 * h;
+                const int g = c / RG;
+                const int row = 32 * (c % RG) + (idx & 3) + 8 * (idx >> 2) + 4 * h;
                 const int64_t t = tbase + row;
                 float L, U;
-                bounds(yv, tq, L, U);
-                const bool keep = idx >= 0 && t < row_end && L <= thr;
-                if (keep) store_cand(L, U, t);
-                const float w = (keep && U < lst[LL - 1]) ? U : INF;
+                bounds(g, yv, tq.v[g], L, U);
+                const bool keep = idx >= 0 && t < row_end && L <= thr[g];
+                if (keep) store_cand(g, L, U, t);
+                const float w = (keep && U < lst[g][LL - 1]) ? U : INF;
                 if constexpr (HALVES) {
                     if (__ballot(w < INF)) {
-                        list_insert(w);
-                        thr = fmin_fast(thr, __builtin_amdgcn_fmed3f(lst[LL - 1], partner(lst[LL - 1]), INF));
+                        list_insert(g, w);
+                        thr[g] = fmin_fast(thr[g], __builtin_amdgcn_fmed3f(lst[g][LL - 1], partner(lst[g][LL - 1]), INF));
                     }
                 } else {
                     // (no lane inserting means no partner inserting: the swap waits for one)
                     if (__ballot(w < INF)) {
                         const float wp = partner(w);  // the other half's candidate
-                        list_insert(w);
-                        list_insert(wp);
-                        thr = fmin_fast(thr, lst[LL - 1]);
+                        list_insert(g, w);
+                        list_insert(g, wp);
+                        thr[g] = fmin_fast(thr[g], lst[g][LL - 1]);
                     }
                 }
             };
             lane_rounds(Y, tf, u, visit);
-            make_tfb();
+#pragma unroll
+            for (int g = 0; g < QG; g++) make_tfb(g);
         }
     };
 
@@ -739,8 +779,8 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             const int64_t t = tbase + row;
             if (p && t < row_end) {
                 float L, U;
-                bounds(y, tq, L, U);
-                if (L <= thr) {
+                bounds(0, y, tq, L, U);
+                if (L <= thr[0]) {
 #pragma unroll
                     for (int i = 0; i < RQ; i++) {
                         qL[i] = i == qcnt ? L : qL[i];
@@ -767,28 +807,102 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         }
     constexpr bool DEFER = NW == 8 && !RL;
     // tile terms (max norm, rounding bound) of the tile in the pipeline (it) and of tile it-1
-    float2 tm_prev = make_float2(0.0f, 0.0f);
+    TQ tm_prev;
+#pragma unroll
+    for (int g = 0; g < QG; g++) tm_prev.v[g] = make_float2(0.0f, 0.0f);
     // study build KNN_STUDY_STAMPS: shader-clock stamps per wave (barrier wait, step, slow path)
     [[maybe_unused]] uint64_t st_bar = 0, st_step = 0, st_slow = 0, st_visits = 0;
     [[maybe_unused]] const uint64_t st_start = KNN_FUSED_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     auto now = [&]() __attribute__((always_inline)) -> uint64_t {
         return KNN_FUSED_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     };
+    // threshold exchanges between the pieces of a query (gthr): every FUSED_SHARE_EVERY tiles
+    // (also after tiles 2, 4, ..., 32 measured no fewer kept rows and B 3 % slower: r04d)
+    auto share_now = [&](int it) __attribute__((always_inline)) {
+        return (it & (FUSED_SHARE_EVERY - 1)) == FUSED_SHARE_EVERY - 1;
+    };
+    // List exchange between the pieces of a query (register-list shapes, a.lshare): a piece's
+    // own list holds the k smallest U of ITS rows only, so the k-th value other pieces publish
+    // through gthr is the k-th best of 1/P of the rows -- with P pieces the threshold trails a
+    // single scan's by a factor P in rank (A's 8-GPU share, P ~ 5: 599 kept rows per query
+    // against 172).  At tiles 32, 64, 128, ... each piece publishes its list (pads as +inf) and
+    // takes the k-th smallest U of the union of every piece's list: a valid bound, as the
+    // pieces' rows are disjoint and every published value is the U of a kept row.  Any value
+    // read may be stale or from a list being rewritten: a list only ever lowers its entries
+    // position by position, so a stale mix counts no more rows below a bound than the current
+    // list holds (a looser bound, never a wrong one).  HALVES: per lane half (its rows), the
+    // bound the larger of the two halves' union values.
+    auto list_share_now = [&](int it) __attribute__((always_inline)) {
+        return it >= 31 && ((it + 1) & it) == 0;
+    };
+    auto exchange_lists = [&]() __attribute__((always_inline)) {
+        if constexpr (RL) {
+            const int W = a.lshare_w;
+#pragma unroll
+            for (int g = 0; g < QG; g++) {
+                float* base = a.lshare + ((qvalid[g] ? q[g] : 0) * (int64_t)a.nseg) * W + (HALVES ? 16 * h : 0);
+                if (qvalid[g] && (HALVES || h == 0)) {
+                    uint32_t* dst = reinterpret_cast<uint32_t*>(base + (int64_t)seg * W);
+#pragma unroll
+                    for (int i = 0; i < LL; i++)
+                        __hip_atomic_store(dst + i, __float_as_uint(lst[g][i] == -INF ? INF : lst[g][i]), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
+                float tmp[LL];
+#pragma unroll
+                for (int i = 0; i < LL; i++) tmp[i] = lst[g][i];
+                for (int p = 0; p < a.nseg; p++) {
+                    if (p == seg) continue;
+                    const uint32_t* src = reinterpret_cast<const uint32_t*>(base + (int64_t)p * W);
+#pragma unroll 1
+                    for (int i0 = 0; i0 < LL; i0 += 4) {
+                        float w[4];
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+                            w[i] = qvalid[g] ? __uint_as_float(__hip_atomic_load(src + i0 + i, __ATOMIC_RELAXED,
+                                                                                 __HIP_MEMORY_SCOPE_AGENT))
+                                             : INF;
+                        // (a published list ascends: past the first value no lane can take, none can)
+                        if (!__ballot(w[0] < tmp[LL - 1])) break;
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const float wi = w[i] < tmp[LL - 1] ? w[i] : INF;
+#pragma unroll
+                            for (int e = LL - 1; e >= 1; e--) tmp[e] = __builtin_amdgcn_fmed3f(tmp[e - 1], wi, tmp[e]);
+                            tmp[0] = fmin_fast(tmp[0], wi);
+                        }
+                    }
+                }
+                const float ub = HALVES ? __builtin_amdgcn_fmed3f(tmp[LL - 1], partner(tmp[LL - 1]), INF) : tmp[LL - 1];
+                if (qvalid[g] && ub < thr[g]) {
+                    thr[g] = ub;
+                    make_tfb(g);
+                }
+            }
+        }
+    };
     auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
-        if ((it & (FUSED_SHARE_EVERY - 1)) == FUSED_SHARE_EVERY - 1) {
+        if constexpr (RL && KNN_FUSED_LIST_SHARE) {
+            if (a.lshare && list_share_now(it)) exchange_lists();
+        }
+        if (share_now(it)) {
             if (a.cursor && threadIdx.x == 0)
                 __hip_atomic_store(&a.cursor[xcd], (uint32_t)(tile_row(it) >> 6), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-            if (a.nseg > 1 && qvalid) {
-                if constexpr (RL) {  // publish this query's bound (the heap path does it per accept)
-                    if (h == 0 && thr < published) {
-                        atomicMin(&a.gthr[q], f2o(thr));
-                        published = thr;
+            if (a.nseg > 1) {
+#pragma unroll
+                for (int g = 0; g < QG; g++) {
+                    if (!qvalid[g]) continue;
+                    if constexpr (RL) {  // publish this query's bound (the heap path does it per accept)
+                        if (h == 0 && thr[g] < published[g]) {
+                            atomicMin(&a.gthr[q[g]], f2o(thr[g]));
+                            published[g] = thr[g];
+                        }
                     }
+                    // thresholds published by other segments of this query
+                    const float gv = o2f(__hip_atomic_load(&a.gthr[q[g]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    if (gv < thr[g]) { thr[g] = gv; make_tfb(g); }
                 }
-                // thresholds published by other segments of this query
-                const float gv = o2f(__hip_atomic_load(&a.gthr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                if (gv < thr) { thr = gv; make_tfb(); }
             }
         }
         // the tiles of this step (both of a pair) have landed -- every wave's pieces: each wave
@@ -802,10 +916,12 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         const uint64_t t1 = now();
         // this tile's terms, for its fast test in the next iteration (the tile is resident:
         // landed before this step's barrier, not overwritten before the next one)
-        const float2 tm_cur = tile_q(it % NBUF);
+        const TQ tm_cur = tile_q(it % NBUF);
         const bool dma_on = !KNN_STUDY_NO_DMA && it + AHEAD < ntiles;
         const DmaTile dd = dma_desc((it + AHEAD) % NBUF, it + AHEAD);
-        const float tf = it > 0 ? tf_of(tm_prev) : -INF;
+        float tf[QG];
+#pragma unroll
+        for (int g = 0; g < QG; g++) tf[g] = it > 0 ? tf_of(g, tm_prev.v[g]) : -INF;
         const uint32_t uY = step(X, Y, it % NBUF, dma_on, dd, tf, PAIR && it % GRP != 0);
         // PAIR: the pair's next tile is resident since its barrier -- its first fragments are
         // read now, so their latency hides under the slow path below
@@ -814,8 +930,8 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         if (!KNN_STUDY_NO_SLOW) {
             if (uY) {
                 if constexpr (RL) slow_rl(Y, it - 1, tf, tm_prev, uY);
-                else if constexpr (DEFER) record(Y, it - 1, tf, tm_prev, uY);
-                else slow(Y, it - 1, tf, tm_prev, uY);
+                else if constexpr (DEFER) record(Y, it - 1, tf[0], tm_prev.v[0], uY);
+                else slow(Y, it - 1, tf[0], tm_prev.v[0], uY);
             }
             if constexpr (DEFER) {
                 if ((it & (FUSED_DEFER_EVERY - 1)) == FUSED_DEFER_EVERY - 1 && __ballot(qcnt > 0)) flush();
@@ -839,22 +955,31 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     if (ntiles > 0) {
         // drain: the last tile's accumulators (ntiles is even: accB)
         const int last = ntiles - 1;
-        const float tf = tf_of(tm_prev);
-        if (pass_set(accB, tf, 0xffffffffu)) {
-            if constexpr (RL) slow_rl(accB, last, tf, tm_prev, 0xffffffffu);
-            else if constexpr (DEFER) record(accB, last, tf, tm_prev, 0xffffffffu);
-            else slow(accB, last, tf, tm_prev, 0xffffffffu);
+        float tf[QG];
+#pragma unroll
+        for (int g = 0; g < QG; g++) tf[g] = tf_of(g, tm_prev.v[g]);
+        if constexpr (RL) {
+            slow_rl(accB, last, tf, tm_prev, 0xffffffffu);
+        } else {
+            if (pass_set(accB, tf[0], 0xffffffffu)) {
+                if constexpr (DEFER) record(accB, last, tf[0], tm_prev.v[0], 0xffffffffu);
+                else slow(accB, last, tf[0], tm_prev.v[0], 0xffffffffu);
+            }
         }
     }
     if constexpr (DEFER) {
         if (__ballot(qcnt > 0)) flush();
     }
     if constexpr (RL) {  // the final bound of this segment, for the other segments' rescore
-        if (a.nseg > 1 && qvalid && h == 0 && thr < published) atomicMin(&a.gthr[q], f2o(thr));
+#pragma unroll
+        for (int g = 0; g < QG; g++)
+            if (a.nseg > 1 && qvalid[g] && h == 0 && thr[g] < published[g]) atomicMin(&a.gthr[q[g]], f2o(thr[g]));
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (qvalid) a.cnt[(int64_t)(2 * seg + h) * a.nq + q] = ccnt;
+#pragma unroll
+    for (int g = 0; g < QG; g++)
+        if (qvalid[g]) a.cnt[(int64_t)(2 * seg + h) * a.nq + q[g]] = ccnt[g];
 #if KNN_FUSED_STAMPS
     {
         if (lane == 0) {
@@ -878,7 +1003,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
 // last round of blocks ends together instead of a partial wave of whole query tiles.
 // Pieces of one query tile share thresholds through gthr like segments (piece id = block -
 // the first block of that query tile).  One call site of fused_piece (instruction cache).
-template <int RB, int MINW, int NBUF, int NW, int RG, int KR>
+template <int RB, int MINW, int NBUF, int NW, int QG, int RG, int KR>
 __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) {
     if ((a.gate && *a.gate == 0) || (*a.status & KNN_STATUS_GEMM_UNSAFE)) return;  // not taken / exact path
     const int64_t T = a.tiles64;  // 64-row units per query tile
@@ -914,7 +1039,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
             adv = t1 - t0;
         }
         if (!first) __syncthreads();  // every wave is done with the previous piece's LDS
-        fused_piece<RB, NBUF, NW, RG, KR>(a, qt, seg, rb, re);
+        fused_piece<RB, NBUF, NW, QG, RG, KR>(a, qt, seg, rb, re);
         x += adv;
     }
 }
@@ -947,8 +1072,8 @@ int knn_fused_schedule(GemmFilterArgs& a, int slots, int* nseg) {
 // ---------------------------------------------------------------------------------
 // plan and launch
 // ---------------------------------------------------------------------------------
-static size_t fused_lds_of(int row_bytes, int k, int nw, int rg, int nbuf, bool heaps) {
-    const int bn = 32 * rg, bm = 32 * nw;
+static size_t fused_lds_of(int row_bytes, int k, int nw, int rg, int nbuf, bool heaps, int qg = 1) {
+    const int bn = 32 * rg, bm = 32 * qg * nw;
     const int hs = row_bytes % 64 == 0 ? bn / 4 + 1 : 0;  // (k_gemm_fused: TN header slots)
     const int ins = (bn * (row_bytes / 16 + 1) + hs + 63) / 64;
     // (+ 16 bytes: the block's scan rotation, k_gemm_fused)
@@ -972,15 +1097,31 @@ int knn_fused_row_bytes(int d) { return d == 64 && KNN_FUSED_AUG64 ? 2 * d + 32 
 //    (C: d = 256, k = 100).
 // Register lists: k <= 16 keeps per-query lists (KR = 16), k <= 32 per-half lists (KR = 32,
 // 16 entries: exact 32-entry lists cost a block per CU of occupancy and 9 % of time on B).
-FilterPlan knn_fused_plan(int d, int k) {
+FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus) {
     const int rb = knn_fused_row_bytes(d);
     const size_t cap = 160 * 1024 - 256;  // room for the kernel's static LDS
     const int kr = k <= 16 ? 16 : k <= 32 ? 32 : 0;
-    auto make = [&](int nw, int rg, int minw, int nbuf) {
-        FilterPlan f{nw, 0, rg, minw, nbuf, 32 * nw, fused_lds_of(rb, k, nw, rg, nbuf, kr == 0)};
+    auto make = [&](int nw, int rg, int minw, int nbuf, int qg = 1) {
+        FilterPlan f{nw, qg, rg, minw, nbuf, 32 * qg * nw, fused_lds_of(rb, k, nw, rg, nbuf, kr == 0, qg)};
         f.kr = kr;
         return f;
     };
+    // Register-list shapes: 64 queries per wave on 32-row tiles (QG = 2: each A fragment read
+    // from LDS feeds two MFMAs, the two accumulators share one norm read, and each tile copy
+    // serves 512 queries -- half the LDS reads and DMA per MFMA) when the 512-query blocks fill
+    // about 3/4 of a round of CUs; fewer queries would cut each query tile into many pieces
+    // (each piece starts its thresholds from +inf), so they keep 32 per wave on 64-row tiles.
+    // Same box (profiles/r04c): A 24.08 -> 23.19 ms, B 575.9 -> 550.9 ms; A's 8-GPU share
+    // (12,500 queries) 3.40 -> 6.33 ms with QG = 2, hence the rule.
+    // KNN_FUSED_QG=1|2 forces the choice (study switch; read per call, tests flip it).
+    const char* qe = getenv("KNN_FUSED_QG");
+    const int qg_env = qe ? atoi(qe) : 0;
+    // (d = 256 keeps 32 queries per wave: two query groups' operands alone are 128 VGPRs)
+    const bool qg2 = d <= 128 && (qg_env == 2 || (qg_env != 1 && nq >= (int64_t)384 * num_cus));
+    // (study switch KNN_FUSED_NBUF=8: QG = 2 tiles in quads -- eight buffers, one barrier per
+    // four 32-row tiles)
+    const char* ne = getenv("KNN_FUSED_NBUF");
+    if (kr > 0 && qg2) return make(8, 1, 2, ne && atoi(ne) == 8 ? 8 : 4, 2);
     if (kr == 0 && d == 64 && fused_lds_of(rb, k, 4, 2, 2, true) <= cap / 2) return make(4, 2, 2, 2);
     if (fused_lds_of(rb, k, 8, 2, 4, kr == 0) <= cap) return make(8, 2, 2, 4);
     if (fused_lds_of(rb, k, 8, 2, 2, kr == 0) <= cap) return make(8, 2, 2, 2);
@@ -990,13 +1131,15 @@ FilterPlan knn_fused_plan(int d, int k) {
 
 template <int RB, int KR>
 static const void* fused_fn_k(const FilterPlan& f) {
-#define KNN_FUSED_FN(NB, NW, RG) reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, NB, NW, RG, KR>)
+#define KNN_FUSED_FN(NB, NW, QG, RG) reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, NB, NW, QG, RG, KR>)
     if constexpr (KR > 0) {
-        return KNN_FUSED_FN(4, 8, 2);  // register lists always fit the pairs shape
+        // register lists always fit the pairs shape
+        if (f.qg == 2) return f.nbuf == 8 ? KNN_FUSED_FN(8, 8, 2, 1) : KNN_FUSED_FN(4, 8, 2, 1);
+        return KNN_FUSED_FN(4, 8, 1, 2);
     } else {
-        if (f.nw == 4) return KNN_FUSED_FN(2, 4, 2);
-        if (f.rg == 2) return f.nbuf == 4 ? KNN_FUSED_FN(4, 8, 2) : KNN_FUSED_FN(2, 8, 2);
-        return KNN_FUSED_FN(2, 8, 1);
+        if (f.nw == 4) return KNN_FUSED_FN(2, 4, 1, 2);
+        if (f.rg == 2) return f.nbuf == 4 ? KNN_FUSED_FN(4, 8, 1, 2) : KNN_FUSED_FN(2, 8, 1, 2);
+        return KNN_FUSED_FN(2, 8, 1, 1);
     }
 #undef KNN_FUSED_FN
 }
@@ -1010,19 +1153,18 @@ static const void* fused_ptr(int d, const FilterPlan& f) {
     return d == 128 ? fused_fn<256>(f) : fused_fn<512>(f);
 }
 
-hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu) {
-    const FilterPlan f = knn_fused_plan(d, k);
+hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu, int64_t nq, int num_cus) {
+    const FilterPlan f = knn_fused_plan(d, k, nq, num_cus);
     if (!knn_fused_supported(d) || f.nw == 0) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fused_ptr(d, f), 64 * f.nw, f.lds);
 }
 
-hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st) {
-    const FilterPlan f = knn_fused_plan(a.d, a.k);
+hipError_t knn_launch_fused(const GemmFilterArgs& a, const FilterPlan& f, hipStream_t st) {
     const int ld = knn_fused_row_bytes(a.d) / 2;  // operand row pitch in elements
     if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != ld || a.ld_q != ld || !a.qstat)
         return hipErrorInvalidValue;
-    if (f.kr > 0 && !(f.nw == 8 && f.rg == 2 &&
-                      f.nbuf == 4))
+    if (f.kr > 0 && !(f.nw == 8 && ((f.nbuf == 4 && f.qg == 1 && f.rg == 2) ||
+                                     ((f.nbuf == 4 || f.nbuf == 8) && f.qg == 2 && f.rg == 1))))
         return hipErrorInvalidValue;  // (fused_fn_k)
     void* args[] = {const_cast<GemmFilterArgs*>(&a)};
     const dim3 grid((unsigned)(a.g2 < 0 ? (int64_t)a.n_qtiles * a.nseg : (int64_t)a.p1_blocks + a.g2));

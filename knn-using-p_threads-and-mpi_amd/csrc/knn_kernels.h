@@ -58,6 +58,9 @@ struct GemmFilterArgs {
     // over the remaining w2 (query tile, 64-row unit) pairs; tiles64 units per query tile
     int p1_blocks; int g2; int64_t w2; int64_t tiles64;
     uint32_t* cursor;       // fused filter, optional: per XCD, the 64-row unit its blocks scan now
+    // fused filter, register-list shapes with nseg > 1 (optional): each piece's threshold list
+    // [nq][nseg][lshare_w] (U values, +inf where empty), shared between a query's pieces
+    float* lshare; int lshare_w;
     const int32_t* status;  // the call's status word: a set GEMM_UNSAFE bit skips the filter
     const int32_t* gate;    // optional: the filter runs only when *gate != 0 (AUTO's re-run)
 };
@@ -153,13 +156,17 @@ hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st);
 // fused-norm filter (knn_fused.hip), d in {64, 128, 256}: train as tile blocks [bn rows rn(t) |
 // bn fp32 norms | tile statistics] (k_tn_rows), each accumulator starting from the norms
 bool knn_fused_supported(int d);
-FilterPlan knn_fused_plan(int d, int k);  // nw == 0: k too large
-hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu);
+// nw == 0: k too large.  nq, num_cus pick the queries per wave (register-list shapes): 64 on
+// 32-row tiles when the queries fill about 3/4 of a round of 512-query blocks, else 32 on 64-row
+// tiles (fewer pieces per query tile)
+FilterPlan knn_fused_plan(int d, int k, int64_t nq = 0, int num_cus = 256);
+hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu, int64_t nq = 0, int num_cus = 256);
 // fills a.p1_blocks / g2 / w2 / tiles64 for the balanced schedule over `slots` resident
 // blocks; returns the grid, *nseg = the most pieces one query tile gets.  (a.g2 = -1 and
 // a.seg_len / nseg instead: the segment schedule, n_qtiles * nseg blocks.)
 int knn_fused_schedule(GemmFilterArgs& a, int slots, int* nseg);
-hipError_t knn_launch_fused(const GemmFilterArgs& a, hipStream_t st);
+// f: the plan run_gemm sized the grid and operands with (knn_fused_plan)
+hipError_t knn_launch_fused(const GemmFilterArgs& a, const FilterPlan& f, hipStream_t st);
 // (study build KNN_STUDY_AUG64 only, d = 64) x [n_valid][ld] (fp32 or bf16) -> bf16 [n][d + 16]:
 // rn(scale * x) | split of norms[r] (or 1 1 1) | 0,
 // and (tstat != NULL, train) the 64-row tile statistics in columns d+8..d+10 of rows 32i;

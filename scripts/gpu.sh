@@ -6,7 +6,8 @@
 #                      same-box bench lines: one bench.py run per spec, its summary printed
 #                      (step, filter, rescore, candidates per query); STEPS / WARMUP per run
 #   STAMPS=<variant>   scripts/stamps.py on build/study/libknn_amd_<variant>.so (a -DKNN_STUDY_STAMPS build)
-#   TESTS=1            the whole -m gpu suite (PYTEST_K narrows it, PYTEST_ENV="VAR=v ..." sets env)
+#   TESTS=1            the whole -m gpu suite (PYTEST_K narrows it, PYTEST_ENV="VAR=v ..." sets env;
+#                      TESTS_ALT_ENV="VAR=v ..." runs it a second time under that env)
 #   BENCHES="A L B"    full bench lines (default steps, CPU baselines on) -> gpurun_out/${TAG}_bench_<cfg>.log
 #   PROFILE="A B C1"   rocprofv3 trace + FETCH/WRITE/SQ passes per workload (scripts/profile_bench.sh),
 #                      outputs gpurun_out/${TAG}_<cfg>_{trace,fetch,write,sq}
@@ -49,6 +50,12 @@ if [ "$TESTS" = 1 ]; then
       ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/${TAG}_pytest_gpu.log 2>&1 \
       || { echo "pytest failed"; tail -30 gpurun_out/${TAG}_pytest_gpu.log; exit 1; }
   tail -1 gpurun_out/${TAG}_pytest_gpu.log
+  if [ -n "$TESTS_ALT_ENV" ]; then  # the suite once more under another study switch
+    env $TESTS_ALT_ENV timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/${TAG}_pytest_gpu_alt.log 2>&1 \
+        || { echo "pytest (alt) failed"; tail -30 gpurun_out/${TAG}_pytest_gpu_alt.log; exit 1; }
+    tail -1 gpurun_out/${TAG}_pytest_gpu_alt.log
+  fi
 fi
 
 for cfg in $BENCHES; do

@@ -116,6 +116,30 @@ def test_train_operands_cached_host_path(knn, oracle):
         ctx.close()
 
 
+@pytest.mark.parametrize("dtype,d,k", [("f32", 64, 32), ("f32", 128, 10), ("f32", 128, 16), ("bf16", 256, 5),
+                                       ("bf16", 64, 24)])
+def test_fused_queries_per_wave_shapes(knn, oracle, dtype, d, k, monkeypatch):
+    """The register-list filter with 32 queries per wave on 64-row tiles (QG = 1) and with 64
+    per wave on 32-row tiles (QG = 2, picked for large query counts): both give the oracle's
+    top-k and predictions bit for bit (main.cpp:40-82), ragged sizes included."""
+    nt, nq = 21_000 + 37, 1_500 + 11
+    train, labels, test = _rows(knn, nt, nq, d, 23, dtype)
+    trf, lab, tef = train.float().cpu().numpy(), labels.cpu().numpy(), test.float().cpu().numpy()
+    qs = np.linspace(0, nq - 1, 40).astype(np.int64)
+    bad, opred, odist, oidx = oracle.knn(trf, lab, tef[qs], k, 10)
+    assert bad == 0
+    out = {}
+    for qg in ("1", "2"):
+        monkeypatch.setenv("KNN_FUSED_QG", qg)
+        c = knn.Context(0, algo="gemm_bf16")
+        out[qg] = _call(c, train, labels, test, k)
+        c.close()
+        assert out[qg][3]["fused_norm"]
+        assert np.array_equal(out[qg][2][qs], oidx) and np.array_equal(out[qg][0][qs], opred)
+        assert np.array_equal(out[qg][1][qs], odist.view(np.uint32))
+    assert _same(out["1"], out["2"])
+
+
 def test_merge_rejects_unsorted_lists(knn):
     import torch
     c = knn.Context(0)
