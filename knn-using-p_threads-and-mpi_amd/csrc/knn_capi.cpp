@@ -483,7 +483,8 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         // filter starts each accumulator from the norms), queries as rn(-2 q) rows; one more
         // tile of pad blocks past the grid (the filter scans tiles in twos, k_gemm_fused).
         // The gated split re-run never takes this branch (the fused filter is the first pass).
-        const int64_t ntf = ntp + 64;
+        const int64_t ntf = ntp + 128;  // (two 64-row tiles of pad blocks: a piece's scan may run
+                                        //  up to three 32-row tiles past its rows, k_gemm_fused)
         const size_t tb = (size_t)bn_f * 2 * d + 4 * bn_f + 16;
         HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * (size_t)d * nq));
         stage_begin(c, st, "aug");
@@ -504,8 +505,8 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         // (study build KNN_STUDY_AUG64, d = 64) augmented bf16 rows: train [rn(t) | tn split],
         // queries [-2 rn(q) | 1 1 1]
         // (pad rows: zero features, a huge norm -- they never pass)
-        // (one more tile of pad rows past the grid: the filter scans tiles in twos, k_gemm_fused)
-        const int64_t ntf = ntp + 64;
+        // (pad rows past the grid: the filter scans tiles in twos, k_gemm_fused)
+        const int64_t ntf = ntp + 128;
         HIP_OR_FAIL(c, c->split_t.ensure(sizeof(uint16_t) * (size_t)(d + 16) * ntf));
         HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * (size_t)(d + 16) * nq));
         stage_begin(c, st, gate ? "aug_rerun" : "aug");
@@ -594,9 +595,12 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         g.cursor = c->cursor.as<uint32_t>();
     }
     // the pieces of a query share their threshold lists, not just their k-th values: the
-    // union's k-th smallest U is the bound a single scan would have (KNN_NO_LIST_SHARE=1: off)
+    // union's k-th smallest U is the bound a single scan would have.  The 32-queries-per-wave
+    // shape only -- the small query counts, whose query tiles are cut into many pieces (A's
+    // 8-GPU share: 5 pieces, 599 -> 447 kept rows per query, filter 3.38 -> 3.19 ms, r04g; on
+    // A and B, 3 and 2 pieces, it measured equal or slower).  KNN_NO_LIST_SHARE=1: off.
     static const bool no_lshare = getenv("KNN_NO_LIST_SHARE") != nullptr;
-    if (fused && !no_lshare && plan.kr > 0 && nseg > 1) {
+    if (fused && !no_lshare && plan.kr > 0 && plan.qg == 1 && nseg > 1) {
         g.lshare_w = plan.kr == 32 ? 32 : 16;
         const int64_t nls = nq * (int64_t)nseg * g.lshare_w;
         HIP_OR_FAIL(c, c->lshare.ensure(sizeof(float) * nls));

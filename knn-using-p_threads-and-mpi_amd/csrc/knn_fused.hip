@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "knn_device.h"
 #include "knn_kernels.h"
@@ -33,7 +34,10 @@ static constexpr int FUSED_DEFER_EVERY = 64;  // 8-wave heap shapes: tiles betwe
 static constexpr int FUSED_SHARE_EVERY = 64;  // tiles between threshold exchanges of a query's pieces (gthr)
 static constexpr int FUSED_RQ = 4;            // queued passing values per lane (heap shapes)
 #ifndef KNN_FUSED_LIST_SHARE
-#define KNN_FUSED_LIST_SHARE 0                // pieces exchange threshold lists (a.lshare)
+#define KNN_FUSED_LIST_SHARE 1                // pieces exchange threshold lists (a.lshare; QG = 1)
+#endif
+#ifndef KNN_FUSED_LIST_EVERY
+#define KNN_FUSED_LIST_EVERY (1 << 30)        // list exchanges: tiles 32, 64, 128, ... (+ every this many)
 #endif
 
 // ---------------------------------------------------------------------------------
@@ -345,7 +349,11 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // copies both accumulator sets -- 32 v_mov -- at every back edge).  The extra tile reads the
     // next BN rows (another piece's, or the padding the train tile blocks carry past the
     // 64-row grid, run_gemm), which the row_end test rejects.
-    const int ntiles = (row_end > row_begin) ? ((int)((row_end - row_begin + BN - 1) / BN) + 1) & ~1 : 0;
+    // (quads: a multiple of four -- the loop runs whole groups, so every tile's place in its
+    // group is a compile-time constant; up to 3 extra tiles, within the two 64-row tiles of pad
+    // blocks past the train grid, run_gemm)
+    constexpr int TSTEP = GRP > 2 ? GRP : 2;
+    const int ntiles = (row_end > row_begin) ? ((int)((row_end - row_begin + BN - 1) / BN) + TSTEP - 1) / TSTEP * TSTEP : 0;
     // Scan order (a.cursor set: the host does so for the multi-segment schedule): the piece's
     // tiles rotated to start where this XCD's other blocks are (per XCD: the 64-row unit the last
     // block to publish was at, if inside this piece) -- so the blocks one XCD runs at once
@@ -833,7 +841,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // list holds (a looser bound, never a wrong one).  HALVES: per lane half (its rows), the
     // bound the larger of the two halves' union values.
     auto list_share_now = [&](int it) __attribute__((always_inline)) {
-        return it >= 31 && ((it + 1) & it) == 0;
+        return (it >= 31 && ((it + 1) & it) == 0) || (it & (KNN_FUSED_LIST_EVERY - 1)) == KNN_FUSED_LIST_EVERY - 1;
     };
     auto exchange_lists = [&]() __attribute__((always_inline)) {
         if constexpr (RL) {
@@ -851,19 +859,23 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                 float tmp[LL];
 #pragma unroll
                 for (int i = 0; i < LL; i++) tmp[i] = lst[g][i];
+                // a published list: +inf at the pad positions [0, pads), then its real values
+                // ascending (+inf where not filled yet) -- reading starts at the chunk holding the
+                // first real value, and a chunk whose smallest value no lane can take ends it
+                const int pads = LL - (HALVES ? (k + 1) / 2 : k);
                 for (int p = 0; p < a.nseg; p++) {
                     if (p == seg) continue;
                     const uint32_t* src = reinterpret_cast<const uint32_t*>(base + (int64_t)p * W);
 #pragma unroll 1
-                    for (int i0 = 0; i0 < LL; i0 += 4) {
+                    for (int i0 = pads & ~3; i0 < LL; i0 += 4) {
                         float w[4];
 #pragma unroll
                         for (int i = 0; i < 4; i++)
                             w[i] = qvalid[g] ? __uint_as_float(__hip_atomic_load(src + i0 + i, __ATOMIC_RELAXED,
                                                                                  __HIP_MEMORY_SCOPE_AGENT))
                                              : INF;
-                        // (a published list ascends: past the first value no lane can take, none can)
-                        if (!__ballot(w[0] < tmp[LL - 1])) break;
+                        const float wmin = fmin_fast(fmin_fast(w[0], w[1]), fmin_fast(w[2], w[3]));
+                        if (!__ballot(wmin < tmp[LL - 1])) break;
 #pragma unroll
                         for (int i = 0; i < 4; i++) {
                             const float wi = w[i] < tmp[LL - 1] ? w[i] : INF;
@@ -881,8 +893,10 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             }
         }
     };
-    auto iter = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
-        if constexpr (RL && KNN_FUSED_LIST_SHARE) {
+    // one tile of the scan; posc: the tile's place in its barrier group (it % GRP), static
+    auto iter = [&](auto posc, floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
+        constexpr int POS = decltype(posc)::value;
+        if constexpr (RL && QG == 1 && KNN_FUSED_LIST_SHARE) {
             if (a.lshare && list_share_now(it)) exchange_lists();
         }
         if (share_now(it)) {
@@ -909,7 +923,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         // waits for all of its own vector-memory ops, then the barrier -- and every wave is done
         // with the buffers the next DMAs overwrite
         const uint64_t t0 = now();
-        if (!PAIR || it % GRP == 0) {
+        if (POS == 0) {
             if constexpr (KNN_STUDY_NO_BARRIER) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             else wait_dma_barrier();
         }
@@ -922,10 +936,10 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         float tf[QG];
 #pragma unroll
         for (int g = 0; g < QG; g++) tf[g] = it > 0 ? tf_of(g, tm_prev.v[g]) : -INF;
-        const uint32_t uY = step(X, Y, it % NBUF, dma_on, dd, tf, PAIR && it % GRP != 0);
+        const uint32_t uY = step(X, Y, it % NBUF, dma_on, dd, tf, POS != 0);
         // PAIR: the pair's next tile is resident since its barrier -- its first fragments are
         // read now, so their latency hides under the slow path below
-        if (PAIR && it % GRP != GRP - 1 && it + 1 < ntiles) prefetch((it + 1) % NBUF);
+        if (POS != GRP - 1 && it + 1 < ntiles) prefetch((it + 1) % NBUF);
         const uint64_t t2 = now();
         if (!KNN_STUDY_NO_SLOW) {
             if (uY) {
@@ -948,9 +962,20 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         }
         tm_prev = tm_cur;
     };
-    for (int it = 0; it < ntiles; it += 2) {
-        iter(accA, accB, it);
-        iter(accB, accA, it + 1);
+    typedef std::integral_constant<int, 0> P0;
+    typedef std::integral_constant<int, 1 % GRP> P1;
+    if constexpr (GRP == 4) {
+        for (int it = 0; it < ntiles; it += 4) {
+            iter(P0{}, accA, accB, it);
+            iter(P1{}, accB, accA, it + 1);
+            iter(std::integral_constant<int, 2>{}, accA, accB, it + 2);
+            iter(std::integral_constant<int, 3>{}, accB, accA, it + 3);
+        }
+    } else {
+        for (int it = 0; it < ntiles; it += 2) {
+            iter(P0{}, accA, accB, it);
+            iter(P1{}, accB, accA, it + 1);
+        }
     }
     if (ntiles > 0) {
         // drain: the last tile's accumulators (ntiles is even: accB)
@@ -1118,10 +1143,11 @@ FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus) {
     const int qg_env = qe ? atoi(qe) : 0;
     // (d = 256 keeps 32 queries per wave: two query groups' operands alone are 128 VGPRs)
     const bool qg2 = d <= 128 && (qg_env == 2 || (qg_env != 1 && nq >= (int64_t)384 * num_cus));
-    // (study switch KNN_FUSED_NBUF=8: QG = 2 tiles in quads -- eight buffers, one barrier per
-    // four 32-row tiles)
+    // (KNN_FUSED_NBUF=4|8 forces pairs or quads for QG = 2: a study switch)
     const char* ne = getenv("KNN_FUSED_NBUF");
-    if (kr > 0 && qg2) return make(8, 1, 2, ne && atoi(ne) == 8 ? 8 : 4, 2);
+    // d = 64: tiles in quads (eight buffers, one barrier per four 32-row tiles: B 546.6 ->
+    // 535.0 ms, r04f); d = 128 in pairs (quads measured equal on A, r04e)
+    if (kr > 0 && qg2) return make(8, 1, 2, ne ? (atoi(ne) == 8 ? 8 : 4) : (d == 64 ? 8 : 4), 2);
     if (kr == 0 && d == 64 && fused_lds_of(rb, k, 4, 2, 2, true) <= cap / 2) return make(4, 2, 2, 2);
     if (fused_lds_of(rb, k, 8, 2, 4, kr == 0) <= cap) return make(8, 2, 2, 4);
     if (fused_lds_of(rb, k, 8, 2, 2, kr == 0) <= cap) return make(8, 2, 2, 2);

@@ -1245,14 +1245,25 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
             umax = max(umax, u);
         }
     }
-    for (int i = RC; i < nreg; i++) {
-        const int e = lane + 64 * i;
-        const int64_t o = position(e);
-        if (e < total) {
-            const uint32_t u = f2o(a.cand[o].U);
-            if (e < su_cap) su[e] = u;
-            umin = min(umin, u);
-            umax = max(umax, u);
+    // batches past RC: their U values in chunks of RCH loads in flight (one round trip per
+    // chunk instead of one per batch: B's 552 rows per query are 9 batches)
+    constexpr int RCH = 4;
+    for (int i0 = RC; i0 < nreg; i0 += RCH) {
+        uint32_t uc[RCH];
+#pragma unroll
+        for (int jj = 0; jj < RCH; jj++) {
+            const int e = lane + 64 * (i0 + jj);
+            const int64_t o = i0 + jj < nreg ? position(e) : 0;  // (uniform: every lane calls it)
+            uc[jj] = (i0 + jj < nreg && e < total) ? f2o(a.cand[o].U) : 0u;
+        }
+#pragma unroll
+        for (int jj = 0; jj < RCH; jj++) {
+            const int e = lane + 64 * (i0 + jj);
+            if (i0 + jj < nreg && e < total) {
+                if (e < su_cap) su[e] = uc[jj];
+                umin = min(umin, uc[jj]);
+                umax = max(umax, uc[jj]);
+            }
         }
     }
 #pragma unroll
@@ -1304,9 +1315,17 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
 #pragma unroll
     for (int i = 0; i < RC; i++)  // static indices: the records stay in registers
         if (i < nreg) compact(i, cr[i]);
-    for (int i = RC; i < nreg; i++) {
-        const int e = lane + 64 * i;
-        compact(i, e < total ? a.cand[position(e)] : CandRec{0, 0.0f, 0.0f});
+    for (int i0 = RC; i0 < nreg; i0 += RCH) {  // (chunks of RCH record loads in flight)
+        CandRec rc[RCH];
+#pragma unroll
+        for (int jj = 0; jj < RCH; jj++) {
+            const int e = lane + 64 * (i0 + jj);
+            const int64_t o = i0 + jj < nreg ? position(e) : 0;
+            rc[jj] = (i0 + jj < nreg && e < total) ? a.cand[o] : CandRec{0, 0.0f, 0.0f};
+        }
+#pragma unroll
+        for (int jj = 0; jj < RCH; jj++)
+            if (i0 + jj < nreg) compact(i0 + jj, rc[jj]);
     }
     if (m > su_cap) {
         if (lane == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = (int32_t)q;

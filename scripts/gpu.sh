@@ -24,7 +24,7 @@ import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);
 sel=d.get('select_stage') or {}
 print(sys.argv[1].split('/')[-1], 'value %.4g'%d['value'], 'step', round(d['ms_per_step'],3), 'filter', s.get('gemm_filter'), 'rescore', s.get('rescore'),
       'norms', s.get('norms'), 'aug', s.get('aug'), 'init', s.get('filter_init'), 'cand/q', sel.get('candidates_per_query'),
-      'fb', d['gemm_stats'].get('fallback_queries'), 'frac', (d.get('roofline') or {}).get('frac'), 'sel_frac', sel.get('frac'))" $1; }
+      'fb', d['gemm_stats'].get('fallback_queries'), 'seg', d['gemm_stats'].get('train_segments'), 'frac', (d.get('roofline') or {}).get('frac'), 'sel_frac', sel.get('frac'))" $1; }
 
 IFS=';' read -ra SPECS <<< "$RUNS"
 for spec in "${SPECS[@]}"; do
