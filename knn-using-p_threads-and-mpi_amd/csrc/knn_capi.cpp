@@ -600,7 +600,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     // 8-GPU share: 5 pieces, 599 -> 447 kept rows per query, filter 3.38 -> 3.19 ms, r04g; on
     // A and B, 3 and 2 pieces, it measured equal or slower).  KNN_NO_LIST_SHARE=1: off.
     static const bool no_lshare = getenv("KNN_NO_LIST_SHARE") != nullptr;
-    if (fused && !no_lshare && plan.kr > 0 && plan.qg == 1 && nseg > 1) {
+    if (fused && !no_lshare && (plan.kr == 16 || plan.kr == 32) && plan.qg == 1 && nseg > 1) {
         g.lshare_w = plan.kr == 32 ? 32 : 16;
         const int64_t nls = nq * (int64_t)nseg * g.lshare_w;
         HIP_OR_FAIL(c, c->lshare.ensure(sizeof(float) * nls));

@@ -19,6 +19,11 @@ typedef unsigned long long u64;
 static inline unsigned elementwise_grid(int64_t total) {
     return (unsigned)std::min<int64_t>((total + 255) / 256, (int64_t)1 << 20);
 }
+// a gated stage (AUTO's re-run, rarely taken) launches at most 2048 blocks of a grid-stride
+// kernel: a re-run not taken then costs a few thousand empty waves, not one per 256 elements
+static inline unsigned gated_grid(unsigned grid, const void* gate) {
+    return gate ? std::min(grid, 2048u) : grid;
+}
 #define KNN_LAUNCH_CHECK() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return e_; } while (0)
 static constexpr u64 KEY_NONE = ~0ull;
 typedef float floatx16 __attribute__((ext_vector_type(16)));

@@ -101,7 +101,7 @@ hipError_t knn_launch_aug_rows(const void* x, int elem, int64_t n, int64_t n_val
     const int64_t total = n * ((d + 16) / 4);
     if (total <= 0) return hipSuccess;
     if (d % 4 || ld % 4) return hipErrorInvalidValue;
-    const dim3 grid(elementwise_grid(total));
+    const dim3 grid(gated_grid(elementwise_grid(total), gate));
     if (elem == ELEM_BF16)
         hipLaunchKernelGGL(k_aug_rows<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, n, n_valid, ld, d, norms, scale,
                            (bf16_t*)out, tstat, gate);
@@ -171,7 +171,7 @@ hipError_t knn_launch_tn_rows(const void* x, int elem, int64_t n, int64_t n_vali
     if (n <= 0) return hipSuccess;
     if (d % 4 || ld % 4 || (norms && (bn <= 0 || n % bn))) return hipErrorInvalidValue;
     const int64_t total = norms ? (n / bn) * ((int64_t)bn * (d / 4) + bn + 1) : n * (d / 4);
-    const dim3 grid(elementwise_grid(total));
+    const dim3 grid(gated_grid(elementwise_grid(total), gate));
     if (elem == ELEM_BF16)
         hipLaunchKernelGGL(k_tn_rows<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, n, n_valid, ld, d, norms, scale,
                            (unsigned char*)out, tstat, bn, gate);
@@ -243,18 +243,17 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     static_assert(NBUF == 2 || NBUF == 4 || NBUF == 8, "tile buffers: two, four (tiles in pairs) or eight (quads)");
     // NBUF = 4: tiles go in pairs -- one barrier per pair; the DMA of tile it + 2 is issued
     // during step it into the buffer tile it - 2 used (read before this pair's barrier)
-    // (quads -- eight buffers, one barrier per four tiles -- and six-buffer pairs with the DMA
-    // two pairs ahead and counted vmcnt waits measured no faster: DESIGN.md, round-3 studies)
+    // NBUF = 8: quads -- one barrier per four tiles (the QG = 2 default, knn_fused_plan)
     constexpr int GRP = NBUF >= 4 ? NBUF / 2 : 1;  // tiles per barrier
     constexpr bool PAIR = GRP > 1;
     constexpr int AHEAD = PAIR ? GRP : NBUF - 1;  // tiles between a step and the tile it DMAs
     static_assert(RG == 1 || RG == 2, "row groups");
-    static_assert(KR == 0 || KR == 16 || KR == 32, "register lists: k <= 16, k <= 32, or LDS heaps");
+    static_assert(KR == 0 || KR == 16 || KR == 32 || KR == 104, "register lists: k <= 16, 32, 104, or LDS heaps");
     constexpr bool RL = KR > 0;                   // thresholds from per-lane register lists (else LDS heaps)
     // (QG = 2 on 64-row tiles, four accumulators, was tried at d = 64: 1.5 KB of scratch spills)
     static_assert(QG == 1 || (QG == 2 && RG == 1 && RL), "64-query waves: 32-row tiles, register lists");
-    constexpr bool HALVES = KR == 32;             // one list per lane half (below): k <= 2 LL
-    constexpr int LL = 16;                        // register list length
+    constexpr bool HALVES = KR >= 32;             // one list per lane half (below): k <= 2 LL
+    constexpr int LL = KR == 104 ? 52 : 16;       // register list length
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* tiles = smem;                                     // [NBUF][TILE]
     const int hs = heap_stride(a.k);
@@ -637,9 +636,9 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // their candidate U (v_permlane32_swap) and both insert both (32 v_med3, the multiset and
     // so the list come out the same in either order): the query's exact k-th smallest, like
     // the heap, for all 32 queries of the wave at once -- no LDS, no lane takes turns.
-    // HALVES (16 < k <= 32, KR = 32): each lane keeps its own
-    // half's ceil(k/2) smallest U (LL - ceil(k/2) pads) and inserts only its own values (LL
-    // v_med3); the bound is the larger of the two
+    // HALVES (16 < k <= 32, KR = 32, LL = 16; 32 < k <= 104, KR = 104, LL = 52): each lane
+    // keeps its own half's ceil(k/2) smallest U (LL - ceil(k/2) pads) and inserts only its own
+    // values (LL v_med3); the bound is the larger of the two
     // halves' ceil(k/2)-th smallest -- at least 2 ceil(k/2) >= k kept rows have U <= it.  A
     // little looser than the exact k-th smallest, with no LDS heap and no turn-taking.
     // (QG = 2: one list per query group.)
@@ -896,7 +895,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // one tile of the scan; posc: the tile's place in its barrier group (it % GRP), static
     auto iter = [&](auto posc, floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
         constexpr int POS = decltype(posc)::value;
-        if constexpr (RL && QG == 1 && KNN_FUSED_LIST_SHARE) {
+        if constexpr (RL && QG == 1 && LL == 16 && KNN_FUSED_LIST_SHARE) {
             if (a.lshare && list_share_now(it)) exchange_lists();
         }
         if (share_now(it)) {
@@ -1125,7 +1124,12 @@ int knn_fused_row_bytes(int d) { return d == 64 && KNN_FUSED_AUG64 ? 2 * d + 32 
 FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus) {
     const int rb = knn_fused_row_bytes(d);
     const size_t cap = 160 * 1024 - 256;  // room for the kernel's static LDS
-    const int kr = k <= 16 ? 16 : k <= 32 ? 32 : 0;
+    // d = 256, 32 < k <= 104 (C): per-half 52-entry register lists instead of LDS heaps, so
+    // the tile buffers get the LDS the heaps held -- 32-row tiles in quads (one barrier per 128
+    // rows) instead of one barrier per 32-row tile (KNN_FUSED_HEAPS=1: the heap shape).  (64-row
+    // tiles in pairs, the other way to the same barrier count, spill: two more accumulators.)
+    const bool force_heaps = getenv("KNN_FUSED_HEAPS") != nullptr;
+    const int kr = k <= 16 ? 16 : k <= 32 ? 32 : (k <= 104 && d == 256 && !force_heaps) ? 104 : 0;
     auto make = [&](int nw, int rg, int minw, int nbuf, int qg = 1) {
         FilterPlan f{nw, qg, rg, minw, nbuf, 32 * qg * nw, fused_lds_of(rb, k, nw, rg, nbuf, kr == 0, qg)};
         f.kr = kr;
@@ -1145,9 +1149,11 @@ FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus) {
     const bool qg2 = d <= 128 && (qg_env == 2 || (qg_env != 1 && nq >= (int64_t)384 * num_cus));
     // (KNN_FUSED_NBUF=4|8 forces pairs or quads for QG = 2: a study switch)
     const char* ne = getenv("KNN_FUSED_NBUF");
-    // d = 64: tiles in quads (eight buffers, one barrier per four 32-row tiles: B 546.6 ->
-    // 535.0 ms, r04f); d = 128 in pairs (quads measured equal on A, r04e)
-    if (kr > 0 && qg2) return make(8, 1, 2, ne ? (atoi(ne) == 8 ? 8 : 4) : (d == 64 ? 8 : 4), 2);
+    // tiles in quads: eight buffers, one barrier per four 32-row tiles, the loop running whole
+    // groups so each tile's place is static (pairs -> quads: B 557.2 -> 501.1 ms, A 22.61 ->
+    // 21.67 ms, r04i; with run-time positions quads measured equal on A, r04e)
+    if (kr > 0 && qg2) return make(8, 1, 2, ne && atoi(ne) == 4 ? 4 : 8, 2);
+    if (kr == 104) return make(8, 1, 2, 8);
     if (kr == 0 && d == 64 && fused_lds_of(rb, k, 4, 2, 2, true) <= cap / 2) return make(4, 2, 2, 2);
     if (fused_lds_of(rb, k, 8, 2, 4, kr == 0) <= cap) return make(8, 2, 2, 4);
     if (fused_lds_of(rb, k, 8, 2, 2, kr == 0) <= cap) return make(8, 2, 2, 2);
@@ -1158,7 +1164,9 @@ FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus) {
 template <int RB, int KR>
 static const void* fused_fn_k(const FilterPlan& f) {
 #define KNN_FUSED_FN(NB, NW, QG, RG) reinterpret_cast<const void*>(&k_gemm_fused<RB, 2, NB, NW, QG, RG, KR>)
-    if constexpr (KR > 0) {
+    if constexpr (KR == 104) {
+        return KNN_FUSED_FN(8, 8, 1, 1);
+    } else if constexpr (KR > 0) {
         // register lists always fit the pairs shape
         if (f.qg == 2) return f.nbuf == 8 ? KNN_FUSED_FN(8, 8, 2, 1) : KNN_FUSED_FN(4, 8, 2, 1);
         return KNN_FUSED_FN(4, 8, 1, 2);
@@ -1171,6 +1179,8 @@ static const void* fused_fn_k(const FilterPlan& f) {
 }
 template <int RB>
 static const void* fused_fn(const FilterPlan& f) {
+    if constexpr (RB == 512)
+        if (f.kr == 104) return fused_fn_k<RB, 104>(f);
     return f.kr == 16 ? fused_fn_k<RB, 16>(f) : f.kr == 32 ? fused_fn_k<RB, 32>(f) : fused_fn_k<RB, 0>(f);
 }
 
@@ -1189,8 +1199,9 @@ hipError_t knn_launch_fused(const GemmFilterArgs& a, const FilterPlan& f, hipStr
     const int ld = knn_fused_row_bytes(a.d) / 2;  // operand row pitch in elements
     if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != ld || a.ld_q != ld || !a.qstat)
         return hipErrorInvalidValue;
-    if (f.kr > 0 && !(f.nw == 8 && ((f.nbuf == 4 && f.qg == 1 && f.rg == 2) ||
-                                     ((f.nbuf == 4 || f.nbuf == 8) && f.qg == 2 && f.rg == 1))))
+    if (f.kr > 0 && !(f.nw == 8 && ((f.nbuf == 4 && f.qg == 1 && f.rg == 2 && f.kr <= 32) ||
+                                     ((f.nbuf == 4 || f.nbuf == 8) && f.qg == 2 && f.rg == 1 && f.kr <= 32) ||
+                                     (f.nbuf == 8 && f.qg == 1 && f.rg == 1 && f.kr == 104 && a.d == 256))))
         return hipErrorInvalidValue;  // (fused_fn_k)
     void* args[] = {const_cast<GemmFilterArgs*>(&a)};
     const dim3 grid((unsigned)(a.g2 < 0 ? (int64_t)a.n_qtiles * a.nseg : (int64_t)a.p1_blocks + a.g2));

@@ -1171,16 +1171,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 // LDS per wave: q row [ld_pad] f32 | counts [C] i32 (C <= KNN_VOTE_LDS_MAX_C) | su [su_cap]
 // ---------------------------------------------------------------------------------
 template <int R, int CAPW, typename E>
-__global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__device__ __forceinline__ void rescore_query(const RescoreArgs& a, const int64_t q, unsigned char* my) {
     const int lane = lane_id();
-    const int wave = threadIdx.x >> 6;
-    unsigned char* my = smem + (size_t)wave * a.wave_lds_bytes;
     float* qs = reinterpret_cast<float*>(my);
     int* counts = a.c_lds_bytes ? reinterpret_cast<int*>(my + a.q_lds_bytes) : nullptr;  // NULL: vote_ballot
     uint32_t* su = reinterpret_cast<uint32_t*>(my + a.q_lds_bytes + a.c_lds_bytes);
-    const int64_t q = (int64_t)blockIdx.x * 4 + wave;
-    if (q >= a.nq) return;
     // sub-slice fills: lane sg < nseg holds slice sg's; inclusive prefix over lanes 0..15.
     // Read before the gate and status words (allocated either way), so the three loads
     // share one round trip.
@@ -1392,6 +1387,25 @@ __global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
     }
     finish_query<R>(T, k, a.C, a.labels, counts, q, a.out, a.status);
 }
+
+// GATED (AUTO's re-run, a.gate set): a bounded grid strides over the queries, so a re-run not
+// taken costs a few thousand empty waves, not nq / 4 blocks.  The ungated instance keeps one
+// query per wave and no loop (the loop in the hot instance cost A 0.26 -> 0.37 ms, r04j).
+template <int R, int CAPW, typename E, bool GATED>
+__global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int wave = threadIdx.x >> 6;
+    unsigned char* my = smem + (size_t)wave * a.wave_lds_bytes;
+    if constexpr (GATED) {
+        if (*a.gate == 0) return;
+        for (int64_t q = (int64_t)blockIdx.x * 4 + wave; q < a.nq; q += (int64_t)gridDim.x * 4)
+            rescore_query<R, CAPW, E>(a, q, my);
+    } else {
+        const int64_t q = (int64_t)blockIdx.x * 4 + wave;
+        if (q < a.nq) rescore_query<R, CAPW, E>(a, q, my);
+    }
+}
+
 
 // ---------------------------------------------------------------------------------
 // k_merge_vote<R>: train-sharded runs.  Each of nsrc train shards gives
@@ -1865,7 +1879,10 @@ static hipError_t launch_rescore_r(const RescoreArgs& a0, hipStream_t st) {
     size_t lds = 4 * (size_t)a.wave_lds_bytes;
     unsigned grid = (unsigned)((a.nq + 3) / 4);
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((k_rescore<R, KNN_RESCORE_CAPW, E>), dim3(grid), dim3(256), lds, st, a);
+    if (a.gate)
+        hipLaunchKernelGGL((k_rescore<R, KNN_RESCORE_CAPW, E, true>), dim3(gated_grid(grid, a.gate)), dim3(256), lds, st, a);
+    else
+        hipLaunchKernelGGL((k_rescore<R, KNN_RESCORE_CAPW, E, false>), dim3(grid), dim3(256), lds, st, a);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -1920,7 +1937,7 @@ hipError_t knn_launch_split_rows(const float* x, int64_t n, int ld, int d, uint1
     const int64_t total = n * (d / 4);
     if (total <= 0) return hipSuccess;
     if (d % 4 || ld % 4) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_split_rows, dim3(elementwise_grid(total)), dim3(256), 0, st, x, n, ld, d, out, gate);
+    hipLaunchKernelGGL(k_split_rows, dim3(gated_grid(elementwise_grid(total), gate)), dim3(256), 0, st, x, n, ld, d, out, gate);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -1930,7 +1947,7 @@ hipError_t knn_launch_round_rows(const float* x, int64_t n, int ld, int d, uint1
     const int64_t total = n * (d / 4);
     if (total <= 0) return hipSuccess;
     if (d % 4 || ld % 4) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_round_rows, dim3(elementwise_grid(total)), dim3(256), 0, st, x, n, ld, d, out, gate);
+    hipLaunchKernelGGL(k_round_rows, dim3(gated_grid(elementwise_grid(total), gate)), dim3(256), 0, st, x, n, ld, d, out, gate);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }
