@@ -78,7 +78,10 @@ typedef struct {
     int32_t device;        /* HIP device ordinal */
     int32_t algo;          /* knn_algo */
     int32_t train_splits;  /* GEMM path: train segments per query tile (0 = auto) */
-    int32_t profile;       /* 1 = record per-stage HIP events (knn_stage_times) */
+    int32_t profile;       /* 1 = record per-stage HIP events (knn_stage_times); 2 = also count the
+                              filter's candidates (an extra read of the counts per call); 3 = events
+                              around the dominant stages only (filter, rescore, direct form, exact
+                              scan, exchange, merge): a few microseconds less per stage skipped */
     int32_t flags;         /* KNN_OPT_* */
 } knn_opts;
 
@@ -222,7 +225,7 @@ knn_status knn_shard_range(int64_t n, int32_t world, int32_t rank, int64_t* begi
 knn_status knn_exchange_layout(int64_t nq, int32_t k, int32_t world, int32_t rank, int64_t* send_off,
                                int64_t* send_cnt, int64_t* recv_off, int64_t* recv_cnt);
 
-/* Per-stage device times (ms) of the last predict call when opts.profile = 1.
+/* Per-stage device times (ms) of the last predict call when opts.profile >= 1.
  * names: optional array of n const char* to receive stage names. Returns the
  * number of stages recorded (<= n). */
 int32_t knn_stage_times(const knn_ctx* ctx, const char** names, float* ms, int32_t n);

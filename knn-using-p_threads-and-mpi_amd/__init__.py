@@ -292,7 +292,8 @@ class Context:
 
     def __init__(self, device=0, algo="auto", train_splits=0, profile=False, cache_train=False):
         self.lib = load_library()
-        # profile: False/0 off, True/1 per-stage HIP events, 2 = also count filter candidates
+        # profile: False/0 off, True/1 per-stage HIP events, 2 = also count filter candidates,
+        # 3 = events around the dominant stages only (filter, rescore, ...: knn_amd.h)
         # cache_train: predict() keeps the device copy of train across calls (KNN_OPT_CACHE_TRAIN)
         opts = knn_opts(device, ALGOS[algo], train_splits, int(profile),
                         KNN_OPT_CACHE_TRAIN if cache_train else 0)

@@ -96,6 +96,7 @@ struct knn_ctx {
     // profiling
     std::vector<hipEvent_t> events;
     std::vector<Stage> stages;
+    bool stage_open = false;  // the last stage_begin recorded an event (profile = 3 skips some)
     std::vector<float> stage_ms;
     std::vector<const char*> stage_names;
     int64_t stats[9] = {0, 0, 0, -1, 0, 0, 0, 0, 0};  // candidates, fallback queries, segments, filter
@@ -136,8 +137,18 @@ knn_status fail(knn_ctx* c, knn_status s, const char* fmt, ...) {
     } while (0)
 
 // profiling helpers: events are created lazily and reused across calls
+// profile = 3: events only around the dominant kernels' stages.  Each event costs the
+// stream a few microseconds: with every stage timed, A's 8-GPU share (12,500 queries) ran
+// 3.44 -> 3.56 ms per step, A 22.58 -> 22.73 (scripts/event_overhead.py, profiles/r04n).
+static bool hot_stage(const char* n) {
+    static const char* const hot[] = {"gemm_filter", "rescore", "direct_tile", "exact_scan", "merge_vote", "exchange"};
+    for (const char* h : hot)
+        if (!strcmp(n, h)) return true;
+    return false;
+}
 void stage_begin(knn_ctx* c, hipStream_t st, const char* name) {
-    if (!c->profile) return;
+    c->stage_open = false;
+    if (!c->profile || (c->profile == 3 && !hot_stage(name))) return;
     size_t i = c->stages.size();
     while (c->events.size() < 2 * (i + 1)) {
         hipEvent_t e;
@@ -147,9 +158,11 @@ void stage_begin(knn_ctx* c, hipStream_t st, const char* name) {
     Stage s{name, c->events[2 * i], c->events[2 * i + 1]};
     c->stages.push_back(s);
     (void)hipEventRecord(s.a, st);
+    c->stage_open = true;
 }
 void stage_end(knn_ctx* c, hipStream_t st) {
-    if (!c->profile || c->stages.empty()) return;
+    if (!c->profile || c->stages.empty() || !c->stage_open) return;
+    c->stage_open = false;
     (void)hipEventRecord(c->stages.back().b, st);
 }
 
@@ -557,6 +570,8 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     }
 
     const FilterPlan plan = fused ? knn_fused_plan(d, k, nq, c->num_cus) : knn_gemm_filter_plan(kelem, rb, k);
+    static const bool no_lshare = getenv("KNN_NO_LIST_SHARE") != nullptr;
+    const bool shared = fused && !no_lshare && knn_fused_list_share_width(plan) > 0;
     const int64_t n_qtiles = (nq + plan.bm - 1) / plan.bm;
     GemmFilterArgs g{};
     g.nt = nt; g.n_qtiles = (int)n_qtiles;
@@ -599,9 +614,8 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     // shape only -- the small query counts, whose query tiles are cut into many pieces (A's
     // 8-GPU share: 5 pieces, 599 -> 447 kept rows per query, filter 3.38 -> 3.19 ms, r04g; on
     // A and B, 3 and 2 pieces, it measured equal or slower).  KNN_NO_LIST_SHARE=1: off.
-    static const bool no_lshare = getenv("KNN_NO_LIST_SHARE") != nullptr;
-    if (fused && !no_lshare && (plan.kr == 16 || plan.kr == 32) && plan.qg == 1 && nseg > 1) {
-        g.lshare_w = plan.kr == 32 ? 32 : 16;
+    if (shared && nseg > 1) {
+        g.lshare_w = knn_fused_list_share_width(plan);
         const int64_t nls = nq * (int64_t)nseg * g.lshare_w;
         HIP_OR_FAIL(c, c->lshare.ensure(sizeof(float) * nls));
         HIP_OR_FAIL(c, knn_launch_fill_u32(c->lshare.as<uint32_t>(), nls, 0x7f800000u, gate, st));  // +inf
@@ -863,7 +877,7 @@ knn_status predict_core(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te
         }
         pass_stats(c, c->ctrl_host, gemm);
     }
-    if (c->profile >= 2 && gemm) {
+    if (c->profile == 2 && gemm) {
         // diagnostic only: total candidates kept by the filter (last pass)
         std::vector<int32_t> h(std::min(pass, te->n) * 2 * c->stats[2]);
         if (hipMemcpy(h.data(), c->cnt.p, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost) == hipSuccess) {

@@ -1104,6 +1104,11 @@ static size_t fused_lds_of(int row_bytes, int k, int nw, int rg, int nbuf, bool 
     return (size_t)nbuf * ins * 1024 + (heaps ? (size_t)bm * heap_stride(k) * sizeof(float) : 0) + 16;
 }
 
+int knn_fused_list_share_width(const FilterPlan& f) {
+    if (!KNN_FUSED_LIST_SHARE || !f.ls || !(f.kr == 16 || f.kr == 32)) return 0;
+    return f.kr == 32 ? 32 : 16;
+}
+
 bool knn_fused_supported(int d) { return d == 64 || d == 128 || d == 256; }
 
 // bytes per operand row in the tile image: 2d -- the accumulators start from the norms in the
@@ -1154,6 +1159,14 @@ FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus) {
     // 21.67 ms, r04i; with run-time positions quads measured equal on A, r04e)
     if (kr > 0 && qg2) return make(8, 1, 2, ne && atoi(ne) == 4 ? 4 : 8, 2);
     if (kr == 104) return make(8, 1, 2, 8);
+    // list exchange between a query's pieces (a.lshare, knn_capi.cpp): the QG = 1 shapes only
+    // (QG = 2 with it: A 21.81 -> 22.84 ms; on A's 8-GPU share, 10 pieces, 3.55 ms against
+    // QG = 1's 3.38 -- more pieces, more kept rows: r04l, r04p)
+    if (kr > 0) {
+        FilterPlan f = make(8, 2, 2, 4);
+        f.ls = 1;
+        return f;
+    }
     if (kr == 0 && d == 64 && fused_lds_of(rb, k, 4, 2, 2, true) <= cap / 2) return make(4, 2, 2, 2);
     if (fused_lds_of(rb, k, 8, 2, 4, kr == 0) <= cap) return make(8, 2, 2, 4);
     if (fused_lds_of(rb, k, 8, 2, 2, kr == 0) <= cap) return make(8, 2, 2, 2);
@@ -1168,7 +1181,9 @@ static const void* fused_fn_k(const FilterPlan& f) {
         return KNN_FUSED_FN(8, 8, 1, 1);
     } else if constexpr (KR > 0) {
         // register lists always fit the pairs shape
-        if (f.qg == 2) return f.nbuf == 8 ? KNN_FUSED_FN(8, 8, 2, 1) : KNN_FUSED_FN(4, 8, 2, 1);
+        if constexpr (RB <= 256) {  // (QG = 2: d <= 128, knn_fused_plan)
+            if (f.qg == 2) return f.nbuf == 8 ? KNN_FUSED_FN(8, 8, 2, 1) : KNN_FUSED_FN(4, 8, 2, 1);
+        }
         return KNN_FUSED_FN(4, 8, 1, 2);
     } else {
         if (f.nw == 4) return KNN_FUSED_FN(2, 4, 1, 2);

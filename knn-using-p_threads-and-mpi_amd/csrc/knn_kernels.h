@@ -139,7 +139,12 @@ bool knn_gemm_filter_supported(int elem, int row_bytes);
 // block shape of the filter for (element type, row bytes, k): waves per block, query
 // groups per wave, row groups per tile, min waves per SIMD (launch bounds), tile buffers,
 // queries per block, LDS bytes per block
-struct FilterPlan { int nw, qg, rg, minw, nbuf, bm; size_t lds; int kr = 0; /* fused: register-list length */ };
+struct FilterPlan {
+    int nw, qg, rg, minw, nbuf, bm;
+    size_t lds;
+    int kr = 0;  // fused: register-list shape (16, 32, 104; 0 = LDS heaps)
+    int ls = 0;  // fused: the kernel exchanges threshold lists between a query's pieces
+};
 FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k);
 hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st);
 size_t knn_gemm_filter_lds(int elem, int row_bytes, int k);
@@ -161,6 +166,8 @@ bool knn_fused_supported(int d);
 // tiles (fewer pieces per query tile)
 FilterPlan knn_fused_plan(int d, int k, int64_t nq = 0, int num_cus = 256);
 hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu, int64_t nq = 0, int num_cus = 256);
+// whether plan f's kernel exchanges threshold lists between a query's pieces (a.lshare, lshare_w floats per piece)
+int knn_fused_list_share_width(const FilterPlan& f);
 // fills a.p1_blocks / g2 / w2 / tiles64 for the balanced schedule over `slots` resident
 // blocks; returns the grid, *nseg = the most pieces one query tile gets.  (a.g2 = -1 and
 // a.seg_len / nseg instead: the segment schedule, n_qtiles * nseg blocks.)

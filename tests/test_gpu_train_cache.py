@@ -140,6 +140,45 @@ def test_fused_queries_per_wave_shapes(knn, oracle, dtype, d, k, monkeypatch):
     assert _same(out["1"], out["2"])
 
 
+@pytest.mark.parametrize("k", [33, 64, 100, 104])
+def test_fused_long_register_lists_vs_heaps(knn, oracle, k, monkeypatch):
+    """d = 256, 32 < k <= 104: the filter keeps per-half 52-entry register lists (32-row tiles
+    in quads) instead of LDS heaps; both shapes give the oracle's top-k and predictions bit for
+    bit (main.cpp:40-82), and each other's.  k = 104 fills the lists (no pad entries)."""
+    nt, nq = 20_000 + 53, 1_200 + 7
+    train, labels, test = _rows(knn, nt, nq, 256, 29, "bf16")
+    trf, lab, tef = train.float().cpu().numpy(), labels.cpu().numpy(), test.float().cpu().numpy()
+    qs = np.linspace(0, nq - 1, 24).astype(np.int64)
+    bad, opred, odist, oidx = oracle.knn(trf, lab, tef[qs], k, 10)
+    assert bad == 0
+    out = {}
+    for heaps in (False, True):
+        if heaps:
+            monkeypatch.setenv("KNN_FUSED_HEAPS", "1")
+        c = knn.Context(0, algo="gemm_bf16")
+        out[heaps] = _call(c, train, labels, test, k)
+        c.close()
+        assert out[heaps][3]["fused_norm"] and out[heaps][3]["fallback_queries"] == 0
+        assert np.array_equal(out[heaps][2][qs], oidx) and np.array_equal(out[heaps][0][qs], opred)
+        assert np.array_equal(out[heaps][1][qs], odist.view(np.uint32))
+    assert _same(out[False], out[True])
+
+
+def test_profile_hot_stages_only(knn):
+    """profile = 3 times only the dominant stages (the filter and the rescore here); profile = 1
+    times every stage; results are the same."""
+    train, labels, test = _rows(knn, 30_000, 2_000, 128, 5)
+    res, names = {}, {}
+    for prof in (1, 3):
+        c = knn.Context(0, algo="gemm_bf16", profile=prof)
+        res[prof] = _call(c, train, labels, test, 10)
+        names[prof] = set(c.stage_times())
+        c.close()
+    assert _same(res[1], res[3])
+    assert {"norms", "gemm_filter", "rescore"} <= names[1]
+    assert names[3] == {"gemm_filter", "rescore"}
+
+
 def test_merge_rejects_unsorted_lists(knn):
     import torch
     c = knn.Context(0)
