@@ -638,6 +638,10 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     r.out = out; r.status = c->ctrl.as<int32_t>();
     r.fb_list = c->fb_list.as<int32_t>(); r.fb_count = c->ctrl.as<int32_t>() + 1;
     r.gate = gate;
+    // the fused filter's final thresholds: the selection stages only the candidates that can
+    // survive (KNN_RESCORE_ALL=1 stages every candidate: a study switch)
+    static const bool rescore_all = getenv("KNN_RESCORE_ALL") != nullptr;
+    r.gthr = fused && !rescore_all ? g.gthr : nullptr;
     // LDS staging for about twice the expected kept rows -- k (1 + ln(nt / k)) for one scan,
     // +25 % per extra segment (they share thresholds through gthr), measured 238 per query on
     // A and 605 on B -- rounded to 64 by the launcher and capped at the list capacity: a

@@ -36,6 +36,9 @@ static constexpr int FUSED_RQ = 4;            // queued passing values per lane 
 #ifndef KNN_FUSED_LIST_SHARE
 #define KNN_FUSED_LIST_SHARE 1                // pieces exchange threshold lists (a.lshare; QG = 1)
 #endif
+#ifndef KNN_FUSED_LIST_FIRST
+#define KNN_FUSED_LIST_FIRST 31               // first list exchange after this tile (then doubling)
+#endif
 #ifndef KNN_FUSED_LIST_EVERY
 #define KNN_FUSED_LIST_EVERY (1 << 30)        // list exchanges: tiles 32, 64, 128, ... (+ every this many)
 #endif
@@ -840,7 +843,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // list holds (a looser bound, never a wrong one).  HALVES: per lane half (its rows), the
     // bound the larger of the two halves' union values.
     auto list_share_now = [&](int it) __attribute__((always_inline)) {
-        return (it >= 31 && ((it + 1) & it) == 0) || (it & (KNN_FUSED_LIST_EVERY - 1)) == KNN_FUSED_LIST_EVERY - 1;
+        return (it >= KNN_FUSED_LIST_FIRST && ((it + 1) & it) == 0) || (it & (KNN_FUSED_LIST_EVERY - 1)) == KNN_FUSED_LIST_EVERY - 1;
     };
     auto exchange_lists = [&]() __attribute__((always_inline)) {
         if constexpr (RL) {
@@ -994,11 +997,15 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     if constexpr (DEFER) {
         if (__ballot(qcnt > 0)) flush();
     }
-    if constexpr (RL) {  // the final bound of this segment, for the other segments' rescore
-#pragma unroll
-        for (int g = 0; g < QG; g++)
-            if (a.nseg > 1 && qvalid[g] && h == 0 && thr[g] < published[g]) atomicMin(&a.gthr[q[g]], f2o(thr[g]));
+    // the final bound of this piece, any segment count: k_rescore stages only the candidates
+    // with L <= gthr (every value there is a k-th smallest U of kept rows, so >= the k-th
+    // smallest U of all of them)
+    if constexpr (!RL) {
+        if (qvalid[0]) thr[0] = fminf(thr[0], root);
     }
+#pragma unroll
+    for (int g = 0; g < QG; g++)
+        if (qvalid[g] && h == 0 && thr[g] < published[g]) atomicMin(&a.gthr[q[g]], f2o(thr[g]));
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll

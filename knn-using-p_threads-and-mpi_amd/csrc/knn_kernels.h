@@ -74,6 +74,10 @@ struct RescoreArgs {
     int32_t* fb_list; int32_t* fb_count;
     const int32_t* gate;  // optional: runs only when *gate != 0 (AUTO's re-run)
     int su_cap;           // candidates staged in LDS per query (host: ~3x the expected count)
+    // optional (the fused filter): per query, an upper bound on the k-th smallest U of its
+    // candidates (ordered float bits, the filter's final thresholds): only candidates with
+    // L <= it can survive, so the selection stages those alone
+    const uint32_t* gthr;
     int q_lds_bytes; int c_lds_bytes; int wave_lds_bytes;  // set by the launcher
 };
 

@@ -1170,8 +1170,27 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 //  * The survivors (L <= threshold) reuse su as their compact index list.
 // LDS per wave: q row [ld_pad] f32 | counts [C] i32 (C <= KNN_VOTE_LDS_MAX_C) | su [su_cap]
 // ---------------------------------------------------------------------------------
+#if KNN_FUSED_STAMPS
+// study build (KNN_STUDY_STAMPS): per-query phase cycles of k_rescore, written (plain vector
+// stores, no shared counter) into a caller's [nq][10] u64 buffer -- [0] fill counts, [1]
+// records staged, [2] bisection, [3] compaction, [4] survivor distances, [5] selection + vote,
+// [6] 1, [7] survivors, [8] record batches, [9] bisection rounds
+__device__ unsigned long long* g_knn_rst_buf;
+__device__ long long g_knn_rst_n;
+extern "C" int knn_debug_rescore_stamps_buffer(void* buf, long long n) {
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_knn_rst_buf), &buf, sizeof(buf)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_knn_rst_n), &n, sizeof(n)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 template <int R, int CAPW, typename E>
 __device__ __forceinline__ void rescore_query(const RescoreArgs& a, const int64_t q, unsigned char* my) {
+    [[maybe_unused]] uint64_t rst[7] = {};
+    [[maybe_unused]] int rounds = 0;
+    auto rstamp = [&](int i) __attribute__((always_inline)) {
+        if constexpr (KNN_FUSED_STAMPS) rst[i] = __builtin_amdgcn_s_memtime();
+    };
+    rstamp(0);
     const int lane = lane_id();
     float* qs = reinterpret_cast<float*>(my);
     int* counts = a.c_lds_bytes ? reinterpret_cast<int*>(my + a.q_lds_bytes) : nullptr;  // NULL: vote_ballot
@@ -1180,6 +1199,8 @@ __device__ __forceinline__ void rescore_query(const RescoreArgs& a, const int64_
     // Read before the gate and status words (allocated either way), so the three loads
     // share one round trip.
     const int cs = lane < a.nseg ? a.cnt[(int64_t)lane * a.nq + q] : 0;
+    // the filter's final bound for this query (ordered bits; the same round trip as the fills)
+    const uint32_t tbits = a.gthr ? a.gthr[__builtin_amdgcn_readfirstlane((int)q)] : 0u;  // (scalar load)
     if (a.gate && *a.gate == 0) return;  // a gated stage (AUTO's re-run) that is not taken
     if (*a.status & KNN_STATUS_GEMM_UNSAFE) {
         // a norm too large for the certificate: every query takes the exact scan
@@ -1197,6 +1218,7 @@ __device__ __forceinline__ void rescore_query(const RescoreArgs& a, const int64_
         if ((lane & 15) >= j) incl += o;
     }
     const int total = __shfl(incl, 15);
+    rstamp(1);
     if (overflow || total < k) {
         if (lane == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = (int32_t)q;
         return;
@@ -1218,181 +1240,306 @@ __device__ __forceinline__ void rescore_query(const RescoreArgs& a, const int64_
     // entries e < su_cap are staged in LDS; a longer list (rare: su_cap is sized ~3x the
     // expected count) re-reads the rest from the candidate arrays in each bisection round
     const int su_cap = a.su_cap;
-    uint32_t umin = 0xffffffffu, umax = 0u;
-    // the first RC batches of records stay in registers: all their loads are issued before
-    // the first use, and the compaction below reads L and idx from them, not memory
-    constexpr int RC = 4;
-    CandRec cr[RC];
-#pragma unroll
-    for (int i = 0; i < RC; i++) {
-        const int e = lane + 64 * i;
-        const int64_t o = position(e);
-        cr[i] = CandRec{0, 0.0f, 0.0f};
-        if (i < nreg && e < total) cr[i] = a.cand[o];
-    }
-#pragma unroll
-    for (int i = 0; i < RC; i++) {
-        const int e = lane + 64 * i;
-        if (i < nreg && e < total) {
-            const uint32_t u = f2o(cr[i].U);
-            if (e < su_cap) su[e] = u;
-            umin = min(umin, u);
-            umax = max(umax, u);
+    int m = 0;
+    [[maybe_unused]] auto rstamps_flush = [&]() __attribute__((always_inline)) {
+#if KNN_FUSED_STAMPS
+        rstamp(6);
+        unsigned long long* o = g_knn_rst_buf;
+        if (o && q < g_knn_rst_n && lane < 10) {
+            const unsigned long long v = lane < 6 ? (unsigned long long)(rst[lane + 1] - rst[lane])
+                                       : lane == 6 ? 1ull : lane == 7 ? (unsigned long long)m
+                                       : lane == 8 ? (unsigned long long)nreg : (unsigned long long)rounds;
+            o[q * 10 + lane] = v;
         }
-    }
-    // batches past RC: their U values in chunks of RCH loads in flight (one round trip per
-    // chunk instead of one per batch: B's 552 rows per query are 9 batches)
-    constexpr int RCH = 4;
-    for (int i0 = RC; i0 < nreg; i0 += RCH) {
-        uint32_t uc[RCH];
+#endif
+    };
+    // survivors' indices in su[0, m): exact distances, selection, vote
+    auto finish_selection = [&](const int m) __attribute__((always_inline)) {
+        u64 T[R];
 #pragma unroll
-        for (int jj = 0; jj < RCH; jj++) {
-            const int e = lane + 64 * (i0 + jj);
-            const int64_t o = i0 + jj < nreg ? position(e) : 0;  // (uniform: every lane calls it)
-            uc[jj] = (i0 + jj < nreg && e < total) ? f2o(a.cand[o].U) : 0u;
-        }
-#pragma unroll
-        for (int jj = 0; jj < RCH; jj++) {
-            const int e = lane + 64 * (i0 + jj);
-            if (i0 + jj < nreg && e < total) {
-                if (e < su_cap) su[e] = uc[jj];
-                umin = min(umin, uc[jj]);
-                umax = max(umax, uc[jj]);
+        for (int r = 0; r < R; r++) T[r] = KEY_NONE;
+        if (m <= 64) {
+            // one batch (the common case): each survivor's rank among the m keys by a scalar
+            // broadcast loop, then one permute puts key r in lane r -- the sorted list without the
+            // bitonic network's 40-odd cross-lane shuffles.  Keys are distinct (the index breaks
+            // ties); an infinite distance gets the key ~0 << 32 | idx (after every finite key,
+            // distinct) and reads KEY_NONE again after the permute.
+            const uint32_t t = lane < m ? su[lane] : 0u;
+            // the survivor's label now: its load lands under the distance's row loads (no
+            // dependent label read after the selection)
+            const int lab = lane < m ? a.labels[t] : -1;
+            u64 key = KEY_NONE;
+            // few survivors: G = d / 32 lanes per row, each row read in one round trip
+            const int G = a.d >> 5;
+            const bool mis = lane < m && ((uintptr_t)(train + (int64_t)t * a.ld_t) & (4 * sizeof(E) - 1)) != 0;
+            // (k <= 32 implies R == 1: the larger lists' instances do not carry its registers)
+            if (R == 1 && (a.d & 31) == 0 && G >= 2 && m * G <= 64 && !__ballot(mis)) {
+                const int r = lane / G, p = lane - r * G;
+                const uint32_t tr = (uint32_t)__shfl((int)t, r < m ? r : 0);
+                const float part = direct_dist_grouped(qs, train + (int64_t)tr * a.ld_t, r < m, p, G);
+                const float dist = __shfl(part, (lane < m ? lane : 0) * G + G - 1);
+                if (lane < m) key = make_key(dist, t);
+            } else if (lane < m) {
+                key = make_key(direct_dist_batched(qs, train + (int64_t)t * a.ld_t, a.d), t);
+            }
+            if (lane < m && key == KEY_NONE) key = 0xffffffff00000000ull | t;
+            if constexpr (KNN_FUSED_STAMPS) {
+                (void)__ballot(key != 0ull);  // (the distances are in registers before the stamp)
+                rstamp(5);
+            }
+            int rank = 0;
+            for (int jj = 0; jj < m; jj++) {
+                const u64 kj = ((u64)__builtin_amdgcn_readlane((uint32_t)(key >> 32), jj) << 32) |
+                               (u64)__builtin_amdgcn_readlane((uint32_t)key, jj);
+                rank += kj < key ? 1 : 0;
+            }
+            const int dst = 4 * (lane < m ? rank : lane);
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)key);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)(key >> 32));
+            T[0] = hi == 0xffffffffu ? KEY_NONE : (((u64)hi << 32) | lo);
+            const int labp = __builtin_amdgcn_ds_permute(dst, lab);
+            finish_query<R>(T, k, a.C, a.labels, counts, q, a.out, a.status, &labp);
+            rstamps_flush();
+            return;
+        } else {
+            rstamp(5);
+            u64 kth = KEY_NONE;
+            for (int b = 0; b < m; b += 64) {
+                u64 key = KEY_NONE;
+                if (b + lane < m) {
+                    const int32_t t = (int32_t)su[b + lane];
+                    key = make_key(direct_dist_batched(qs, train + (int64_t)t * a.ld_t, a.d), (uint32_t)t);
+                }
+                const bool pass = key < kth;
+                if (__ballot(pass)) {
+                    topk_merge<R>(T, pass ? key : KEY_NONE);
+                    kth = list_at(T, k - 1);
+                }
             }
         }
-    }
+        finish_query<R>(T, k, a.C, a.labels, counts, q, a.out, a.status);
+        rstamps_flush();
+    };
+    // Staged selection (the fused filter: a.gthr).  tb = the filter's final bound for this
+    // query, >= the k-th smallest U of all its candidates; a candidate with L > tb cannot
+    // survive (a true neighbour has L <= D <= D_(k) <= tb), and every candidate with U <= the
+    // k-th smallest U has L <= tb, so the k-th smallest U of the staged set is the same value.
+    // One pass over the records stages {U, L, idx} of those (B: ~90 of ~550) in LDS; the
+    // bisection and the survivors then work on at most 4 register batches of them.  More than
+    // CS staged: the general path below (every candidate's U in su).
+    const int CS = min(4 * 64, (su_cap / 3) & ~63);
+    bool staged = false;
+    if (a.gthr && CS >= 64) {
+        const float tb = o2f(tbits);
+        uint32_t* cu = su;
+        float* cl = reinterpret_cast<float*>(su + CS);
+        int32_t* ci = reinterpret_cast<int32_t*>(su + 2 * CS);
+        int nc = 0;
+        constexpr int RS = 4;  // record batches in flight per chunk
+        for (int i0 = 0; i0 < nreg; i0 += RS) {
+            CandRec rc[RS];
 #pragma unroll
-    for (int j = 32; j > 0; j >>= 1) {
-        umin = min(umin, (uint32_t)__shfl_xor((int)umin, j));
-        umax = max(umax, (uint32_t)__shfl_xor((int)umax, j));
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    // the threshold: the smallest x with #{U <= x} >= k, or any x above it -- every x >= it
-    // is a valid bound (it only admits more survivors) -- so the bisection stops at 2^10
-    // ordered-float steps (2^-13 relative), far inside the certificate's band
-    // the register-resident batches count from their own U bits (no LDS round trip per round)
-    uint32_t ur[RC];
+            for (int jj = 0; jj < RS; jj++) {
+                const int e = lane + 64 * (i0 + jj);
+                const int64_t o = i0 + jj < nreg ? position(e) : 0;  // (uniform: every lane calls it)
+                rc[jj] = (i0 + jj < nreg && e < total) ? a.cand[o] : CandRec{0, 0.0f, 0.0f};
+            }
 #pragma unroll
-    for (int i = 0; i < RC; i++) ur[i] = (i < nreg && lane + 64 * i < total) ? f2o(cr[i].U) : 0xffffffffu;
-    uint32_t lo = umin, hi = umax;
-    while (hi - lo > 1024u) {
-        const uint32_t mid = lo + ((hi - lo) >> 1);
-        int c = 0;
-#pragma unroll
-        for (int i = 0; i < RC; i++)
-            if (i < nreg) c += __popcll(__ballot(lane + 64 * i < total && ur[i] <= mid));
-        for (int i = RC; i < nreg; i++) {
-            const int e = lane + 64 * i;
-            // position() shuffles across the wave: every lane calls it (wave-uniform branch)
-            const int64_t o = 64 * i + 63 >= su_cap ? position(e) : 0;
-            uint32_t u = 0xffffffffu;
-            if (e < total) u = e < su_cap ? su[e] : f2o(a.cand[o].U);
-            c += __popcll(__ballot(e < total && u <= mid));
+            for (int jj = 0; jj < RS; jj++) {
+                if (i0 + jj >= nreg) break;
+                const int e = lane + 64 * (i0 + jj);
+                const bool pass = e < total && rc[jj].L <= tb;
+                const u64 bal = __ballot(pass);
+                const int slot = nc + __popcll(bal & ((1ull << lane) - 1ull));
+                if (pass && slot < CS) {
+                    cu[slot] = f2o(rc[jj].U);
+                    cl[slot] = rc[jj].L;
+                    ci[slot] = rc[jj].idx;
+                }
+                nc += __popcll(bal);
+            }
         }
-        if (c >= k) hi = mid; else lo = mid + 1;
+        if (nc <= CS && nc >= k) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            const int nbc = (nc + 63) >> 6;
+            uint32_t ub[4];
+            float lb[4];
+            int32_t ib[4];
+            uint32_t cmin = 0xffffffffu, cmax = 0u;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const int e = lane + 64 * b;
+                const bool v = b < nbc && e < nc;
+                ub[b] = v ? cu[e] : 0xffffffffu;
+                lb[b] = v ? cl[e] : __uint_as_float(0x7f800000u);
+                ib[b] = v ? ci[e] : 0;
+                cmin = min(cmin, ub[b]);
+                cmax = v ? max(cmax, ub[b]) : cmax;
+            }
+#pragma unroll
+            for (int j = 32; j > 0; j >>= 1) {
+                cmin = min(cmin, (uint32_t)__shfl_xor((int)cmin, j));
+                cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, j));
+            }
+            rstamp(2);
+            uint32_t lo = cmin, hi = cmax;
+            while (hi - lo > 1024u) {
+                const uint32_t mid = lo + ((hi - lo) >> 1);
+                int c = 0;
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    if (b < nbc) c += __popcll(__ballot(ub[b] <= mid));
+                if (c >= k) hi = mid; else lo = mid + 1;
+                if constexpr (KNN_FUSED_STAMPS) rounds++;
+            }
+            const float thr = o2f(hi);
+            rstamp(3);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();  // every staged entry is in registers: su is free
+            m = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                if (b >= nbc) break;
+                const bool sv = lb[b] <= thr;
+                const u64 bal = __ballot(sv);
+                const int slot = m + __popcll(bal & ((1ull << lane) - 1ull));
+                if (sv) su[slot] = (uint32_t)ib[b];
+                m += __popcll(bal);
+            }
+            staged = true;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // (su is rewritten below)
     }
-    const float thr = o2f(hi);
-    // compact survivors L <= thr into su (a write never overtakes an unread entry; more
-    // survivors than su holds -- pathological ties -- send the query to the exact scan)
-    int m = 0;
-    auto compact = [&](int i, const CandRec& r) __attribute__((always_inline)) {
-        const int e = lane + 64 * i;
-        const bool sv = e < total && r.L <= thr;
-        const int32_t t = sv ? r.idx : 0;
-        const u64 bal = __ballot(sv);
+    // General path: every candidate's U staged in su (entries past su_cap re-read), the
+    // bisection over all of them, then the survivors.
+    if (!staged) {
+        uint32_t umin = 0xffffffffu, umax = 0u;
+        // the first RC batches of records stay in registers: all their loads are issued before
+        // the first use, and the compaction below reads L and idx from them, not memory
+        constexpr int RC = 4;
+        CandRec cr[RC];
+#pragma unroll
+        for (int i = 0; i < RC; i++) {
+            const int e = lane + 64 * i;
+            const int64_t o = position(e);
+            cr[i] = CandRec{0, 0.0f, 0.0f};
+            if (i < nreg && e < total) cr[i] = a.cand[o];
+        }
+#pragma unroll
+        for (int i = 0; i < RC; i++) {
+            const int e = lane + 64 * i;
+            if (i < nreg && e < total) {
+                const uint32_t u = f2o(cr[i].U);
+                if (e < su_cap) su[e] = u;
+                umin = min(umin, u);
+                umax = max(umax, u);
+            }
+        }
+        // batches past RC: their U values in chunks of RCH loads in flight (one round trip per
+        // chunk instead of one per batch: B's 552 rows per query are 9 batches)
+        constexpr int RCH = 4;
+        for (int i0 = RC; i0 < nreg; i0 += RCH) {
+            uint32_t uc[RCH];
+#pragma unroll
+            for (int jj = 0; jj < RCH; jj++) {
+                const int e = lane + 64 * (i0 + jj);
+                const int64_t o = i0 + jj < nreg ? position(e) : 0;  // (uniform: every lane calls it)
+                uc[jj] = (i0 + jj < nreg && e < total) ? f2o(a.cand[o].U) : 0u;
+            }
+#pragma unroll
+            for (int jj = 0; jj < RCH; jj++) {
+                const int e = lane + 64 * (i0 + jj);
+                if (i0 + jj < nreg && e < total) {
+                    if (e < su_cap) su[e] = uc[jj];
+                    umin = min(umin, uc[jj]);
+                    umax = max(umax, uc[jj]);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 32; j > 0; j >>= 1) {
+            umin = min(umin, (uint32_t)__shfl_xor((int)umin, j));
+            umax = max(umax, (uint32_t)__shfl_xor((int)umax, j));
+        }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        const int slot = m + __popcll(bal & ((1ull << lane) - 1ull));
-        if (sv && slot < su_cap) su[slot] = (uint32_t)t;
-        m += __popcll(bal);
-    };
+        rstamp(2);
+        // the threshold: the smallest x with #{U <= x} >= k, or any x above it -- every x >= it
+        // is a valid bound (it only admits more survivors) -- so the bisection stops at 2^10
+        // ordered-float steps (2^-13 relative), far inside the certificate's band
+        // the register-resident batches count from their own U bits (no LDS round trip per round)
+        uint32_t ur[RC];
 #pragma unroll
-    for (int i = 0; i < RC; i++)  // static indices: the records stay in registers
-        if (i < nreg) compact(i, cr[i]);
-    for (int i0 = RC; i0 < nreg; i0 += RCH) {  // (chunks of RCH record loads in flight)
-        CandRec rc[RCH];
+        for (int i = 0; i < RC; i++) ur[i] = (i < nreg && lane + 64 * i < total) ? f2o(cr[i].U) : 0xffffffffu;
+        uint32_t lo = umin, hi = umax;
+        while (hi - lo > 1024u) {
+            const uint32_t mid = lo + ((hi - lo) >> 1);
+            int c = 0;
 #pragma unroll
-        for (int jj = 0; jj < RCH; jj++) {
-            const int e = lane + 64 * (i0 + jj);
-            const int64_t o = i0 + jj < nreg ? position(e) : 0;
-            rc[jj] = (i0 + jj < nreg && e < total) ? a.cand[o] : CandRec{0, 0.0f, 0.0f};
-        }
-#pragma unroll
-        for (int jj = 0; jj < RCH; jj++)
-            if (i0 + jj < nreg) compact(i0 + jj, rc[jj]);
-    }
-    if (m > su_cap) {
-        if (lane == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = (int32_t)q;
-        return;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-
-    u64 T[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) T[r] = KEY_NONE;
-    if (m <= 64) {
-        // one batch (the common case): each survivor's rank among the m keys by a scalar
-        // broadcast loop, then one permute puts key r in lane r -- the sorted list without the
-        // bitonic network's 40-odd cross-lane shuffles.  Keys are distinct (the index breaks
-        // ties); an infinite distance gets the key ~0 << 32 | idx (after every finite key,
-        // distinct) and reads KEY_NONE again after the permute.
-        const uint32_t t = lane < m ? su[lane] : 0u;
-        // the survivor's label now: its load lands under the distance's row loads (no
-        // dependent label read after the selection)
-        const int lab = lane < m ? a.labels[t] : -1;
-        u64 key = KEY_NONE;
-        // few survivors: G = d / 32 lanes per row, each row read in one round trip
-        const int G = a.d >> 5;
-        const bool mis = lane < m && ((uintptr_t)(train + (int64_t)t * a.ld_t) & (4 * sizeof(E) - 1)) != 0;
-        // (k <= 32 implies R == 1: the larger lists' instances do not carry its registers)
-        if (R == 1 && (a.d & 31) == 0 && G >= 2 && m * G <= 64 && !__ballot(mis)) {
-            const int r = lane / G, p = lane - r * G;
-            const uint32_t tr = (uint32_t)__shfl((int)t, r < m ? r : 0);
-            const float part = direct_dist_grouped(qs, train + (int64_t)tr * a.ld_t, r < m, p, G);
-            const float dist = __shfl(part, (lane < m ? lane : 0) * G + G - 1);
-            if (lane < m) key = make_key(dist, t);
-        } else if (lane < m) {
-            key = make_key(direct_dist_batched(qs, train + (int64_t)t * a.ld_t, a.d), t);
-        }
-        if (lane < m && key == KEY_NONE) key = 0xffffffff00000000ull | t;
-        int rank = 0;
-        for (int jj = 0; jj < m; jj++) {
-            const u64 kj = ((u64)__builtin_amdgcn_readlane((uint32_t)(key >> 32), jj) << 32) |
-                           (u64)__builtin_amdgcn_readlane((uint32_t)key, jj);
-            rank += kj < key ? 1 : 0;
-        }
-        const int dst = 4 * (lane < m ? rank : lane);
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)key);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)(key >> 32));
-        T[0] = hi == 0xffffffffu ? KEY_NONE : (((u64)hi << 32) | lo);
-        const int labp = __builtin_amdgcn_ds_permute(dst, lab);
-        finish_query<R>(T, k, a.C, a.labels, counts, q, a.out, a.status, &labp);
-        return;
-    } else {
-        u64 kth = KEY_NONE;
-        for (int b = 0; b < m; b += 64) {
-            u64 key = KEY_NONE;
-            if (b + lane < m) {
-                const int32_t t = (int32_t)su[b + lane];
-                key = make_key(direct_dist_batched(qs, train + (int64_t)t * a.ld_t, a.d), (uint32_t)t);
+            for (int i = 0; i < RC; i++)
+                if (i < nreg) c += __popcll(__ballot(lane + 64 * i < total && ur[i] <= mid));
+            for (int i = RC; i < nreg; i++) {
+                const int e = lane + 64 * i;
+                // position() shuffles across the wave: every lane calls it (wave-uniform branch)
+                const int64_t o = 64 * i + 63 >= su_cap ? position(e) : 0;
+                uint32_t u = 0xffffffffu;
+                if (e < total) u = e < su_cap ? su[e] : f2o(a.cand[o].U);
+                c += __popcll(__ballot(e < total && u <= mid));
             }
-            const bool pass = key < kth;
-            if (__ballot(pass)) {
-                topk_merge<R>(T, pass ? key : KEY_NONE);
-                kth = list_at(T, k - 1);
-            }
+            if (c >= k) hi = mid; else lo = mid + 1;
+            if constexpr (KNN_FUSED_STAMPS) rounds++;
         }
+        const float thr = o2f(hi);
+        rstamp(3);
+        // compact survivors L <= thr into su (a write never overtakes an unread entry; more
+        // survivors than su holds -- pathological ties -- send the query to the exact scan)
+        m = 0;
+        auto compact = [&](int i, const CandRec& r) __attribute__((always_inline)) {
+            const int e = lane + 64 * i;
+            const bool sv = e < total && r.L <= thr;
+            const int32_t t = sv ? r.idx : 0;
+            const u64 bal = __ballot(sv);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            const int slot = m + __popcll(bal & ((1ull << lane) - 1ull));
+            if (sv && slot < su_cap) su[slot] = (uint32_t)t;
+            m += __popcll(bal);
+        };
+#pragma unroll
+        for (int i = 0; i < RC; i++)  // static indices: the records stay in registers
+            if (i < nreg) compact(i, cr[i]);
+        for (int i0 = RC; i0 < nreg; i0 += RCH) {  // (chunks of RCH record loads in flight)
+            CandRec rc[RCH];
+#pragma unroll
+            for (int jj = 0; jj < RCH; jj++) {
+                const int e = lane + 64 * (i0 + jj);
+                const int64_t o = i0 + jj < nreg ? position(e) : 0;
+                rc[jj] = (i0 + jj < nreg && e < total) ? a.cand[o] : CandRec{0, 0.0f, 0.0f};
+            }
+#pragma unroll
+            for (int jj = 0; jj < RCH; jj++)
+                if (i0 + jj < nreg) compact(i0 + jj, rc[jj]);
+        }
+        if (m > su_cap) {
+            if (lane == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = (int32_t)q;
+            return;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
-    finish_query<R>(T, k, a.C, a.labels, counts, q, a.out, a.status);
+    rstamp(4);
+    finish_selection(m);
 }
 
 // GATED (AUTO's re-run, a.gate set): a bounded grid strides over the queries, so a re-run not
 // taken costs a few thousand empty waves, not nq / 4 blocks.  The ungated instance keeps one
 // query per wave and no loop (the loop in the hot instance cost A 0.26 -> 0.37 ms, r04j).
+// (6 waves per SIMD for the k <= 512 instances: the staged selection left the f32 k <= 64
+// instance at 81 VGPRs, one over the 6-wave budget)
 template <int R, int CAPW, typename E, bool GATED>
-__global__ __launch_bounds__(256) void k_rescore(RescoreArgs a) {
+__global__ __launch_bounds__(256, (R <= 8 && !GATED) ? 6 : 1) void k_rescore(RescoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = threadIdx.x >> 6;
     unsigned char* my = smem + (size_t)wave * a.wave_lds_bytes;

@@ -4,6 +4,8 @@
 # objects of everything else.  Select it with KNN_AMD_LIB=<path> (the package's loader).
 #   bash scripts/build_variant.sh base HEAD              -> build/study/libknn_amd_base.so
 #   bash scripts/build_variant.sh stamps . -DKNN_STUDY_STAMPS
+# KERNELS=1: knn_kernels.hip (rescore, direct form, ...) from the same revision with the same
+# flags too (e.g. the rescore's phase stamps, knn_debug_rescore_stamps).
 set -e
 NAME=$1; REV=$2; shift 2
 P=$(cd "$(dirname "$0")/../knn-using-p_threads-and-mpi_amd" && pwd)
@@ -14,6 +16,14 @@ SRC=csrc/.variant_${NAME}.hip
 if [ "$REV" = "." ]; then cp csrc/knn_fused.hip $SRC; else git show "$REV:knn-using-p_threads-and-mpi_amd/csrc/knn_fused.hip" > $SRC; fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" -c -o build/study/knn_fused_$NAME.o $SRC
 rm -f $SRC
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/study/libknn_amd_$NAME.so build/knn_kernels.o \
+KOBJ=build/knn_kernels.o
+if [ "$KERNELS" = 1 ]; then
+  KSRC=csrc/.variant_k_${NAME}.hip
+  if [ "$REV" = "." ]; then cp csrc/knn_kernels.hip $KSRC; else git show "$REV:knn-using-p_threads-and-mpi_amd/csrc/knn_kernels.hip" > $KSRC; fi
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" -c -o build/study/knn_kernels_$NAME.o $KSRC
+  rm -f $KSRC
+  KOBJ=build/study/knn_kernels_$NAME.o
+fi
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/study/libknn_amd_$NAME.so $KOBJ \
     build/study/knn_fused_$NAME.o build/knn_capi.o build/knn_comm.o build/knn_arff.o build/knn_build_id.o -ldl
 echo "built build/study/libknn_amd_$NAME.so"
