@@ -1123,14 +1123,15 @@ bool knn_fused_supported(int d) { return d == 64 || d == 128 || d == 256; }
 // (2d + 32) stays as the study build KNN_STUDY_AUG64
 int knn_fused_row_bytes(int d) { return d == 64 && KNN_FUSED_AUG64 ? 2 * d + 32 : 2 * d; }
 
-// Shapes (d = features; rows of 2d + 32 bytes).  Block = NW waves x 32 queries:
-//  * k <= 32 (register lists, KR = 16 / 32): 8 waves, 64-row tiles in pairs (four buffers,
-//    one barrier per two tiles) -- measured on A: 33.4 -> 31.3 ms against two buffers; B
-//    (d = 64): 765 ms with 4-wave blocks, 743 with 8 (256 queries share a tile's DMA).
-//  * k > 32 (LDS heaps, KR = 0): d = 64 in 4-wave blocks, two buffers, two blocks per CU
-//    (the other block hides the per-tile barrier and fast test of 5-step tiles); d >= 128 in
-//    8-wave blocks: pairs when they fit beside the heaps, else two buffers, else 32-row tiles
-//    (C: d = 256, k = 100).
+// Shapes (d = features; rows of 2d bytes).  Block = NW waves x 32 QG queries:
+//  * k <= 32 (register lists, KR = 16 / 32): 8 waves; 64 queries per wave on 32-row tiles in
+//    quads for large query counts (below), else 32 per wave on 64-row tiles -- in quads when
+//    eight buffers fit (d <= 128), else in pairs (four buffers, one barrier per two tiles:
+//    A 33.4 -> 31.3 ms against two buffers, round 2; 8-wave blocks: B 765 -> 743 ms).
+//  * d = 256, 32 < k <= 104 (KR = 104): 8 waves, 32-row tiles in quads.
+//  * k > 32 otherwise (LDS heaps, KR = 0): d = 64 in 4-wave blocks, two buffers, two blocks per
+//    CU (the other block hides the per-tile barrier and fast test of 5-step tiles); d >= 128 in
+//    8-wave blocks: pairs when they fit beside the heaps, else two buffers, else 32-row tiles.
 // Register lists: k <= 16 keeps per-query lists (KR = 16), k <= 32 per-half lists (KR = 32,
 // 16 entries: exact 32-entry lists cost a block per CU of occupancy and 9 % of time on B).
 FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus) {
@@ -1159,7 +1160,7 @@ FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus) {
     const int qg_env = qe ? atoi(qe) : 0;
     // (d = 256 keeps 32 queries per wave: two query groups' operands alone are 128 VGPRs)
     const bool qg2 = d <= 128 && (qg_env == 2 || (qg_env != 1 && nq >= (int64_t)384 * num_cus));
-    // (KNN_FUSED_NBUF=4|8 forces pairs or quads for QG = 2: a study switch)
+    // (KNN_FUSED_NBUF=4 forces pairs for the register-list shapes: a study switch)
     const char* ne = getenv("KNN_FUSED_NBUF");
     // tiles in quads: eight buffers, one barrier per four 32-row tiles, the loop running whole
     // groups so each tile's place is static (pairs -> quads: B 557.2 -> 501.1 ms, A 22.61 ->
@@ -1170,7 +1171,10 @@ FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus) {
     // (QG = 2 with it: A 21.81 -> 22.84 ms; on A's 8-GPU share, 10 pieces, 3.55 ms against
     // QG = 1's 3.38 -- more pieces, more kept rows: r04l, r04p)
     if (kr > 0) {
-        FilterPlan f = make(8, 2, 2, 4);
+        // 64-row tiles in quads when eight buffers fit (d <= 128): A's 8-GPU share 3.08 -> 2.96 ms,
+        // A at QG = 1 23.05 -> 22.31 (r04u); KNN_FUSED_NBUF=4 forces pairs (a study switch)
+        const bool q8 = !(ne && atoi(ne) == 4) && fused_lds_of(rb, k, 8, 2, 8, false) <= cap;
+        FilterPlan f = make(8, 2, 2, q8 ? 8 : 4);
         f.ls = 1;
         return f;
     }
@@ -1191,7 +1195,7 @@ static const void* fused_fn_k(const FilterPlan& f) {
         if constexpr (RB <= 256) {  // (QG = 2: d <= 128, knn_fused_plan)
             if (f.qg == 2) return f.nbuf == 8 ? KNN_FUSED_FN(8, 8, 2, 1) : KNN_FUSED_FN(4, 8, 2, 1);
         }
-        return KNN_FUSED_FN(4, 8, 1, 2);
+        return f.nbuf == 8 ? KNN_FUSED_FN(8, 8, 1, 2) : KNN_FUSED_FN(4, 8, 1, 2);
     } else {
         if (f.nw == 4) return KNN_FUSED_FN(2, 4, 1, 2);
         if (f.rg == 2) return f.nbuf == 4 ? KNN_FUSED_FN(4, 8, 1, 2) : KNN_FUSED_FN(2, 8, 1, 2);
@@ -1221,7 +1225,7 @@ hipError_t knn_launch_fused(const GemmFilterArgs& a, const FilterPlan& f, hipStr
     const int ld = knn_fused_row_bytes(a.d) / 2;  // operand row pitch in elements
     if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != ld || a.ld_q != ld || !a.qstat)
         return hipErrorInvalidValue;
-    if (f.kr > 0 && !(f.nw == 8 && ((f.nbuf == 4 && f.qg == 1 && f.rg == 2 && f.kr <= 32) ||
+    if (f.kr > 0 && !(f.nw == 8 && (((f.nbuf == 4 || f.nbuf == 8) && f.qg == 1 && f.rg == 2 && f.kr <= 32) ||
                                      ((f.nbuf == 4 || f.nbuf == 8) && f.qg == 2 && f.rg == 1 && f.kr <= 32) ||
                                      (f.nbuf == 8 && f.qg == 1 && f.rg == 1 && f.kr == 104 && a.d == 256))))
         return hipErrorInvalidValue;  // (fused_fn_k)
