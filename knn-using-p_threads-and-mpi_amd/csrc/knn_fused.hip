@@ -1195,7 +1195,10 @@ static const void* fused_fn_k(const FilterPlan& f) {
         if constexpr (RB <= 256) {  // (QG = 2: d <= 128, knn_fused_plan)
             if (f.qg == 2) return f.nbuf == 8 ? KNN_FUSED_FN(8, 8, 2, 1) : KNN_FUSED_FN(4, 8, 2, 1);
         }
-        return f.nbuf == 8 ? KNN_FUSED_FN(8, 8, 1, 2) : KNN_FUSED_FN(4, 8, 1, 2);
+        if constexpr (RB <= 256) {  // (quads of 64-row tiles: d <= 128, knn_fused_plan)
+            if (f.nbuf == 8) return KNN_FUSED_FN(8, 8, 1, 2);
+        }
+        return KNN_FUSED_FN(4, 8, 1, 2);
     } else {
         if (f.nw == 4) return KNN_FUSED_FN(2, 4, 1, 2);
         if (f.rg == 2) return f.nbuf == 4 ? KNN_FUSED_FN(4, 8, 1, 2) : KNN_FUSED_FN(2, 8, 1, 2);
@@ -1211,7 +1214,10 @@ static const void* fused_fn(const FilterPlan& f) {
 }
 
 static const void* fused_ptr(int d, const FilterPlan& f) {
-    if (d == 64) return KNN_FUSED_AUG64 ? fused_fn<160>(f) : fused_fn<128>(f);
+    if (d == 64) {
+        if constexpr (KNN_FUSED_AUG64) return fused_fn<160>(f);
+        else return fused_fn<128>(f);
+    }
     return d == 128 ? fused_fn<256>(f) : fused_fn<512>(f);
 }
 
