@@ -36,6 +36,9 @@ static constexpr int FUSED_RQ = 4;            // queued passing values per lane 
 #ifndef KNN_FUSED_LIST_SHARE
 #define KNN_FUSED_LIST_SHARE 1                // pieces exchange threshold lists (a.lshare; QG = 1)
 #endif
+#ifndef KNN_FUSED_FORWARD
+#define KNN_FUSED_FORWARD 0                   // balanced ranges in range order (study; default: from the end)
+#endif
 #ifndef KNN_FUSED_LIST_FIRST
 #define KNN_FUSED_LIST_FIRST 31               // first list exchange after this tile (then doubling)
 #endif
@@ -1050,6 +1053,12 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
         x1 = p1 ? x + T : lo(b2 + 1);
     }
     const int qbase = p1 ? 0 : a.p1_blocks;
+    // A range runs from its END: the head of its later query tile first (from train row 0),
+    // then the tail of the earlier one.  At time tau every block of the balanced schedule is
+    // then near train tile tau (or tau + T - W after its switch), so the blocks stream the
+    // train rows together through the L2s and the Infinity Cache; in range order each would
+    // start from its own row, all 260 MB of A's train operand in use at once, cycling through
+    // a 256 MiB cache.  (KNN_FUSED_FORWARD=1: range order, a study build.)
     for (bool first = true; x < x1; first = false) {
         int qt, seg;
         int64_t rb, re, adv;
@@ -1060,8 +1069,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
             re = min(a.nt, rb + a.seg_len);
             adv = 1;
         } else {
+#if KNN_FUSED_FORWARD
             const int64_t ql = x / T, t0 = x - ql * T;
             const int64_t t1 = min(T, t0 + (x1 - x));
+#else
+            const int64_t ql = (x1 - 1) / T;
+            const int64_t t0 = max(x, ql * T) - ql * T, t1 = x1 - ql * T;
+#endif
             qt = qbase + (int)ql;
             // the block whose range holds the query tile's first unit: largest bb with lo(bb) <= ql T
             seg = p1 ? 0 : (int)(b2 - ((ql * T + 1) * a.g2 - 1) / a.w2);
@@ -1071,7 +1085,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_fused(GemmFilterArgs a) 
         }
         if (!first) __syncthreads();  // every wave is done with the previous piece's LDS
         fused_piece<RB, NBUF, NW, QG, RG, KR>(a, qt, seg, rb, re);
-        x += adv;
+        if (KNN_FUSED_FORWARD || segmode) x += adv;
+        else x1 -= adv;
     }
 }
 
