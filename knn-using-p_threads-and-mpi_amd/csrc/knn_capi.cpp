@@ -496,8 +496,8 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         // filter starts each accumulator from the norms), queries as rn(-2 q) rows; one more
         // tile of pad blocks past the grid (the filter scans tiles in twos, k_gemm_fused).
         // The gated split re-run never takes this branch (the fused filter is the first pass).
-        const int64_t ntf = ntp + 256;  // (four 64-row tiles of pad blocks: a piece's scan may run
-                                        //  up to three tiles past its rows, k_gemm_fused's quads)
+        const int64_t ntf = ntp + 256;  // (256 pad rows: a piece's scan may run up to 224 rows past
+                                        //  its own -- seven 32-row tiles of an octet, k_gemm_fused)
         const size_t tb = (size_t)bn_f * 2 * d + 4 * bn_f + 16;
         HIP_OR_FAIL(c, c->split_q.ensure(sizeof(uint16_t) * (size_t)d * nq));
         stage_begin(c, st, "aug");

@@ -246,10 +246,12 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     constexpr int DMA_PER_WAVE = (DMA_INS + NW - 1) / NW;
     constexpr int NS = RB / 32;                  // k-steps: d/16 feature steps (+ the norm step)
     constexpr int VPS = (16 + NS - 1) / NS;      // fast-test values per k-step per accumulator
-    static_assert(NBUF == 2 || NBUF == 4 || NBUF == 8, "tile buffers: two, four (tiles in pairs) or eight (quads)");
+    static_assert(NBUF == 2 || NBUF == 4 || NBUF == 8 || NBUF == 16, "tile buffers: two, four (pairs), eight (quads), 16 (octets)");
     // NBUF = 4: tiles go in pairs -- one barrier per pair; the DMA of tile it + 2 is issued
     // during step it into the buffer tile it - 2 used (read before this pair's barrier)
-    // NBUF = 8: quads -- one barrier per four tiles (the QG = 2 default, knn_fused_plan)
+    // NBUF = 8: quads -- one barrier per four tiles; NBUF = 16: octets (the QG = 2 default,
+    // knn_fused_plan: eight 32-row tiles per barrier; the code of eight static tile places is
+    // ~50 KB)
     constexpr int GRP = NBUF >= 4 ? NBUF / 2 : 1;  // tiles per barrier
     constexpr bool PAIR = GRP > 1;
     constexpr int AHEAD = PAIR ? GRP : NBUF - 1;  // tiles between a step and the tile it DMAs
@@ -969,7 +971,18 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     };
     typedef std::integral_constant<int, 0> P0;
     typedef std::integral_constant<int, 1 % GRP> P1;
-    if constexpr (GRP == 4) {
+    if constexpr (GRP == 8) {  // octets (the 64-query shape's default)
+        for (int it = 0; it < ntiles; it += 8) {
+            iter(P0{}, accA, accB, it);
+            iter(P1{}, accB, accA, it + 1);
+            iter(std::integral_constant<int, 2>{}, accA, accB, it + 2);
+            iter(std::integral_constant<int, 3>{}, accB, accA, it + 3);
+            iter(std::integral_constant<int, 4>{}, accA, accB, it + 4);
+            iter(std::integral_constant<int, 5>{}, accB, accA, it + 5);
+            iter(std::integral_constant<int, 6>{}, accA, accB, it + 6);
+            iter(std::integral_constant<int, 7>{}, accB, accA, it + 7);
+        }
+    } else if constexpr (GRP == 4) {
         for (int it = 0; it < ntiles; it += 4) {
             iter(P0{}, accA, accB, it);
             iter(P1{}, accB, accA, it + 1);
@@ -1140,7 +1153,7 @@ int knn_fused_row_bytes(int d) { return d == 64 && KNN_FUSED_AUG64 ? 2 * d + 32 
 
 // Shapes (d = features; rows of 2d bytes).  Block = NW waves x 32 QG queries:
 //  * k <= 32 (register lists, KR = 16 / 32): 8 waves; 64 queries per wave on 32-row tiles in
-//    quads for large query counts (below), else 32 per wave on 64-row tiles -- in quads when
+//    octets for large query counts (below), else 32 per wave on 64-row tiles -- in quads when
 //    eight buffers fit (d <= 128), else in pairs (four buffers, one barrier per two tiles:
 //    A 33.4 -> 31.3 ms against two buffers, round 2; 8-wave blocks: B 765 -> 743 ms).
 //  * d = 256, 32 < k <= 104 (KR = 104): 8 waves, 32-row tiles in quads.
@@ -1177,10 +1190,14 @@ FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus) {
     const bool qg2 = d <= 128 && (qg_env == 2 || (qg_env != 1 && nq >= (int64_t)384 * num_cus));
     // (KNN_FUSED_NBUF=4 forces pairs for the register-list shapes: a study switch)
     const char* ne = getenv("KNN_FUSED_NBUF");
-    // tiles in quads: eight buffers, one barrier per four 32-row tiles, the loop running whole
+    // tiles in octets: 16 buffers, one barrier per eight 32-row tiles, the loop running whole
     // groups so each tile's place is static (pairs -> quads: B 557.2 -> 501.1 ms, A 22.61 ->
-    // 21.67 ms, r04i; with run-time positions quads measured equal on A, r04e)
-    if (kr > 0 && qg2) return make(8, 1, 2, ne && atoi(ne) == 4 ? 4 : 8, 2);
+    // 21.67 ms, r04i; quads -> octets: A 21.49 -> 20.80 ms, B 504.6 -> 483.8 ms, r04y).
+    // KNN_FUSED_NBUF=4|8 forces pairs or quads (a study switch).
+    if (kr > 0 && qg2) {
+        const int nb = ne && atoi(ne) == 4 ? 4 : ne && atoi(ne) == 8 ? 8 : 16;
+        return make(8, 1, 2, fused_lds_of(rb, k, 8, 1, nb, false, 2) <= cap ? nb : 8, 2);
+    }
     if (kr == 104) return make(8, 1, 2, 8);
     // list exchange between a query's pieces (a.lshare, knn_capi.cpp): the QG = 1 shapes only
     // (QG = 2 with it: A 21.81 -> 22.84 ms; on A's 8-GPU share, 10 pieces, 3.55 ms against
@@ -1208,7 +1225,8 @@ static const void* fused_fn_k(const FilterPlan& f) {
     } else if constexpr (KR > 0) {
         // register lists always fit the pairs shape
         if constexpr (RB <= 256) {  // (QG = 2: d <= 128, knn_fused_plan)
-            if (f.qg == 2) return f.nbuf == 8 ? KNN_FUSED_FN(8, 8, 2, 1) : KNN_FUSED_FN(4, 8, 2, 1);
+            if (f.qg == 2)
+                return f.nbuf == 16 ? KNN_FUSED_FN(16, 8, 2, 1) : f.nbuf == 8 ? KNN_FUSED_FN(8, 8, 2, 1) : KNN_FUSED_FN(4, 8, 2, 1);
         }
         if constexpr (RB <= 256) {  // (quads of 64-row tiles: d <= 128, knn_fused_plan)
             if (f.nbuf == 8) return KNN_FUSED_FN(8, 8, 1, 2);
@@ -1247,7 +1265,7 @@ hipError_t knn_launch_fused(const GemmFilterArgs& a, const FilterPlan& f, hipStr
     if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != ld || a.ld_q != ld || !a.qstat)
         return hipErrorInvalidValue;
     if (f.kr > 0 && !(f.nw == 8 && (((f.nbuf == 4 || f.nbuf == 8) && f.qg == 1 && f.rg == 2 && f.kr <= 32) ||
-                                     ((f.nbuf == 4 || f.nbuf == 8) && f.qg == 2 && f.rg == 1 && f.kr <= 32) ||
+                                     ((f.nbuf == 4 || f.nbuf == 8 || f.nbuf == 16) && f.qg == 2 && f.rg == 1 && f.kr <= 32) ||
                                      (f.nbuf == 8 && f.qg == 1 && f.rg == 1 && f.kr == 104 && a.d == 256))))
         return hipErrorInvalidValue;  // (fused_fn_k)
     void* args[] = {const_cast<GemmFilterArgs*>(&a)};
