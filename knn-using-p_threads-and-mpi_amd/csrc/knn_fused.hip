@@ -523,11 +523,15 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // append candidate (L, U) of global row t to query group g's sub-slice of this lane half
     // (past its capacity: counted only, the rescore then sends the query to the exact scan)
     auto store_cand = [&](int g, float L, float U, int64_t t) __attribute__((always_inline)) {
+#ifndef KNN_STUDY_NO_STORE
         if (ccnt[g] < cap_sub) {
             const int64_t o = q[g] * (int64_t)a.cap + (int64_t)(2 * seg + h) * cap_sub + ccnt[g];
             a.cand[o] = CandRec{(int32_t)t, L, U};
         }
         ccnt[g]++;
+#else  // (ablation build: no candidate stores, nothing counted -- every query takes the exact scan)
+        asm volatile("" ::"v"(L), "v"(U), "v"((int)t));
+#endif
     };
     // (heap shapes, QG = 1) keep candidate (L, U) of global row t: the exact test against the
     // current threshold, the candidate store into this lane half's sub-slice, and, if U beats
