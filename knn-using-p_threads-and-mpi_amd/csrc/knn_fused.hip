@@ -356,9 +356,9 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // copies both accumulator sets -- 32 v_mov -- at every back edge).  The extra tile reads the
     // next BN rows (another piece's, or the padding the train tile blocks carry past the
     // 64-row grid, run_gemm), which the row_end test rejects.
-    // (quads: a multiple of four -- the loop runs whole groups, so every tile's place in its
-    // group is a compile-time constant; up to 3 extra tiles, within the two 64-row tiles of pad
-    // blocks past the train grid, run_gemm)
+    // (quads / octets: a multiple of four / eight -- the loop runs whole groups, so every tile's
+    // place in its group is a compile-time constant; up to 7 extra 32-row tiles, within the 256
+    // pad rows past the train grid, run_gemm)
     constexpr int TSTEP = GRP > 2 ? GRP : 2;
     const int ntiles = (row_end > row_begin) ? ((int)((row_end - row_begin + BN - 1) / BN) + TSTEP - 1) / TSTEP * TSTEP : 0;
     // Scan order (a.cursor set: the host does so for the multi-segment schedule): the piece's
