@@ -47,18 +47,18 @@
     } while (0)
 #endif
 
-// The fused filter's instruction order inside a k-step (knn_fused.hip, step()): a full
-// scheduling barrier after every k-step keeps each step's A-fragment prefetch, DMA piece,
-// MFMAs and fast-test VALU together -- a performance choice only: correctness rests on the
-// tile barrier retiring every LDS read (wait_dma_barrier), and the free schedule passes the
-// parity suite.  KNN_FUSED_FREE_SCHEDULE (study) lets the compiler schedule across
-// the steps.
-#ifdef KNN_FUSED_FREE_SCHEDULE
+// The fused filter's instruction order inside a k-step (knn_fused.hip, step()): the compiler
+// schedules across the k-steps (round 4, octets: A 21.33 -> 21.08 ms, B equal, r04ae).  The
+// order is a performance choice only: correctness rests on the tile barrier retiring every LDS
+// read (wait_dma_barrier).  KNN_FUSED_STRICT_SCHEDULE (study) puts a full scheduling barrier
+// after every k-step (each step's A-fragment prefetch, DMA piece, MFMAs and fast-test VALU
+// kept together: the round-2/3 default).
+#ifdef KNN_FUSED_STRICT_SCHEDULE
+#define KNN_FUSED_KSTEP_ORDER() __builtin_amdgcn_sched_barrier(0)
+#else
 #define KNN_FUSED_KSTEP_ORDER() \
     do {                        \
     } while (0)
-#else
-#define KNN_FUSED_KSTEP_ORDER() __builtin_amdgcn_sched_barrier(0)
 #endif
 
 // KNN_STUDY_STAMPS: per-wave shader-clock stamps of the fused filter's loop (barrier wait, step,
