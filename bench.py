@@ -154,6 +154,48 @@ def cpu_baseline_arff(k, threads=None):
     return rec
 
 
+def oracle_bit_match(seed, kind, nt, d, k, C, q_rows, got_pred, threads=None, chunk=1 << 20):
+    """The bench run proves its own result (metric: "...; accuracy bit-match"): the
+    predictions the timed steps produced for a spread sample of global query rows q_rows
+    against the C oracle (oracle/knn_oracle.c, main.cpp:25-85) over the WHOLE train set,
+    regenerated on the host from the same counter-based generator in chunks of `chunk` rows:
+    each chunk's exact top-k (the oracle's stable insertion), merged by (distance bits,
+    global index) -- the reference's lower-index tie rule -- then the vote (smallest label on
+    ties).  Runs after the timed region; the oracle is the checker only."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from conftest import Oracle
+    o = Oracle()
+    threads = threads or int(os.environ.get("KNN_BENCH_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    t0 = time.perf_counter()
+    te = np.concatenate([o.gen(seed, 1, int(q), 1, d, kind=kind, C=C)[0] for q in q_rows])
+    nq = len(q_rows)
+    best_d = np.zeros((nq, 0), np.uint32)
+    best_i = np.zeros((nq, 0), np.int64)
+    best_l = np.zeros((nq, 0), np.int32)
+    for r0 in range(0, nt, chunk):
+        n = min(chunk, nt - r0)
+        tr, tl = o.gen(seed, 0, r0, n, d, kind=kind, C=C)
+        bad, _, dist, idx = o.knn(tr, tl, te, min(k, n), C, threads=threads)
+        ok = idx >= 0
+        lab = np.where(ok, tl[np.clip(idx, 0, n - 1)], -1)
+        best_d = np.concatenate([best_d, dist.view(np.uint32)], axis=1)
+        best_i = np.concatenate([best_i, np.where(ok, idx.astype(np.int64) + r0, -1)], axis=1)
+        best_l = np.concatenate([best_l, lab], axis=1)
+        keep_d, keep_i, keep_l = [], [], []
+        for q in range(nq):
+            v = best_i[q] >= 0
+            order = np.lexsort((best_i[q][v], best_d[q][v]))[:k]
+            keep_d.append(best_d[q][v][order]); keep_i.append(best_i[q][v][order]); keep_l.append(best_l[q][v][order])
+        best_d, best_i, best_l = np.stack(keep_d), np.stack(keep_i), np.stack(keep_l)
+        del tr, tl
+    want = np.array([int(np.argmax(np.bincount(best_l[q], minlength=C))) for q in range(nq)], np.int32)
+    got = np.asarray(got_pred, np.int32)
+    return {"predictions_equal_oracle": bool(np.array_equal(got, want)), "queries_checked": int(nq),
+            "mismatches": int((got != want).sum()), "query_rows": [int(q) for q in q_rows[:4]] + ["..."],
+            "checker": "oracle/knn_oracle.c over the whole train set (host-regenerated, chunked, merged)",
+            "check_s": round(time.perf_counter() - t0, 1)}
+
+
 def bench_arff(args, knn, torch, local):
     """configs[1]: the reference's large ARFF pair, k = 5, inputs resident in HBM."""
     nt, nq, d, k, C = CONFIGS["L"][:5]
@@ -306,6 +348,13 @@ def main():
     ap.add_argument("--nq", type=int, default=0, help="override query rows (kernel studies)")
     ap.add_argument("--no-train-cache", action="store_true",
                     help="recompute the train-side filter operands (norms, tile blocks) in every step")
+    ap.add_argument("--shard", default=None, choices=["test", "train", "auto"],
+                    help="partition over ranks: test-sharded (train replicated), train-sharded (RCCL "
+                         "exchange + merge) or auto (knn_shard_policy); default: the config's own")
+    ap.add_argument("--no-uncached", action="store_true",
+                    help="skip the extra steps that time a context without the train-operand cache")
+    ap.add_argument("--no-bit-match", action="store_true",
+                    help="skip the oracle check of a sample of this run's predictions")
     args = ap.parse_args()
     if args.steps is None:
         args.steps = DEFAULT_STEPS[args.config]
@@ -341,6 +390,15 @@ def main():
 
     nt, nq_cfg, d, k, C, seed, scaling, dtype, sharding = CONFIGS[args.config]
     nt, nq_cfg = args.nt or nt, args.nq or nq_cfg
+    # the partition: the config's own (BASELINE configs: A/B test-sharded, C train-sharded), or
+    # --shard test|train, or --shard auto = knn_shard_policy (north_star's rule: replicate train
+    # while it fits one GPU, else shard it)
+    shard_req = args.shard or sharding
+    if args.shard == "auto":
+        sharding = knn.shard_policy(nt, nq_cfg, d, dtype, world,
+                                    torch.cuda.get_device_properties(local).total_memory)
+    elif args.shard:
+        sharding = args.shard
     if args.weak and sharding == "test":
         scaling = "weak"
     kind = 1 if dtype == "bf16" else 0                  # bf16-exact generator values for bf16
@@ -432,6 +490,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     stats = ctx.stats()
+    pred_timed = pred.clone()  # the timed steps' predictions (bit_match below checks these)
     # select stage (k_rescore): one untimed diagnostic pass counts the filter's candidates,
     # giving the rescore's algorithmic bytes (select stage vs HBM)
     select = None
@@ -458,6 +517,39 @@ def main():
                   "candidates_per_query": round(cand / nq, 1), "algorithmic_bytes": byts,
                   "achieved": round(byts / (resc_ms * 1e-3) / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
                   "frac": round(byts / (resc_ms * 1e-3) / 1e9 / 8000.0, 4)}
+    # the same step with the train-side operands rebuilt in every step (a context without
+    # KNN_OPT_CACHE_TRAIN: the reference's one-shot KNN(train, test, k) pays this pass,
+    # main.cpp:25-43) -- reported beside value, never as it
+    uncached_ms = None
+    if not args.no_train_cache and not args.no_uncached:
+        ctx.close()
+        ctx = knn.Context(local, algo=args.algo, train_splits=args.splits, profile=0, cache_train=False)
+        if comm is not None:
+            comm.ctx = ctx
+        step()  # workspace allocation
+        n_unc = 3 if 1e3 * elapsed / args.steps < 100 else 1
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_u = time.perf_counter()
+        for _ in range(n_unc):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tu = torch.tensor([time.perf_counter() - t_u], dtype=torch.float64, device="cpu" if share else dev)
+        if world > 1:
+            dist.all_reduce(tu, op=dist.ReduceOp.MAX)
+        uncached_ms = 1e3 * float(tu.item()) / n_unc
+    # bit-match of this run's own predictions (rank 0's queries, a spread sample) against the
+    # oracle over the whole train set
+    bitm = None
+    if rank == 0 and not args.no_bit_match:
+        own_q0 = q0 if sharding == "test" else knn.shard_range(nq, world, rank)[0]
+        pl = pred_timed.cpu().numpy()
+        n_s = 64 if float(nt) * d <= 2.1e9 else 8
+        pos = np.unique(np.linspace(0, len(pl) - 1, min(n_s, len(pl))).astype(np.int64))
+        bitm = oracle_bit_match(seed, kind, nt, d, k, C, own_q0 + pos, pl[pos])
     host = None
     if rank == 0 and world == 1 and sharding == "test" and not args.no_host_path:
         host = host_buffer_times(knn, local, args.algo, train, labels, test, k, C, pred)
@@ -514,7 +606,7 @@ def main():
             "config": {"workload": f"{args.config}: synthetic {nt} train x {nq_cfg} query"
                                    f"{'/GPU' if scaling == 'weak' else ''} x {d}-d {dtype}, k={k}",
                        "n_train": nt, "n_query_total": total_q, "d": d, "k": k, "classes": C,
-                       "parallelism": par},
+                       "parallelism": par, "shard": {"requested": shard_req, "used": sharding}},
             "queries_per_s": total_q * args.steps / elapsed,
             "stages_ms": {n: round(v, 3) for n, v in stages.items()},
             "stages_source": ("timed steps for " + ", ".join(sorted(stage_sum)) +
@@ -523,6 +615,9 @@ def main():
             "predictions_gathered": gathered,
             "rccl_comm_ranks": rccl_ranks,
             "pmc_key": pmc_key,
+            "ms_per_step_uncached": None if uncached_ms is None else round(uncached_ms, 3),
+            "value_uncached": None if uncached_ms is None else pairs / args.steps / (uncached_ms * 1e-3),
+            "bit_match": bitm,
             "train_operands": ("cached across steps (KNN_OPT_CACHE_TRAIN: norms, tile statistics and bf16 "
                                "tile blocks built in the warmup step)" if stats.get("train_operands_cached")
                                else "rebuilt every step"),

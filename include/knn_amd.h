@@ -29,7 +29,9 @@
 extern "C" {
 #endif
 
-#define KNN_AMD_ABI_VERSION 2
+/* 3: KNN_OPT_CACHE_TRAIN no longer reuses operands derived from a caller's DEVICE train buffer;
+ *    that is the separate opt-in KNN_OPT_CACHE_TRAIN_DEVICE (ABI 2 did it under the one flag) */
+#define KNN_AMD_ABI_VERSION 3
 
 typedef enum {
     KNN_OK = 0,
@@ -66,12 +68,19 @@ typedef enum {
 /* knn_opts.flags */
 #define KNN_OPT_CACHE_TRAIN 1  /* knn_predict keeps the device copy of train across calls, keyed
                                   by (feat, labels, n, d, ld, dtype) and the generation set by
-                                  knn_set_generation; every entry point also keeps the train-side
-                                  operands of the bf16 MFMA filter (train norms, tile statistics,
-                                  bf16 tile blocks) across calls, keyed by (feat, n, d, ld, dtype,
-                                  filter tile height) and the generation -- a caller that rewrites
-                                  a train buffer in place (or frees it and reuses the address)
-                                  bumps the generation */
+                                  knn_set_generation, together with the train-side operands of
+                                  the bf16 MFMA filter derived from that copy (train norms, tile
+                                  statistics, bf16 tile blocks) */
+#define KNN_OPT_CACHE_TRAIN_DEVICE 2  /* (with KNN_OPT_CACHE_TRAIN) the device entry points
+                                  (knn_predict_device, knn_shard_topk_device,
+                                  knn_predict_train_sharded) also keep the filter operands derived
+                                  from the CALLER's device train buffer, keyed by (feat, n, d, ld,
+                                  dtype, filter tile height) and the generation.  The library
+                                  cannot see writes to that buffer: a caller that rewrites it in
+                                  place (hipMemcpy, its own kernels) or frees it and reuses the
+                                  address must bump the generation (knn_set_generation) before
+                                  the next call, or it gets results for the old rows.  Without
+                                  this flag every device call rebuilds them (A: ~0.3 ms) */
 
 /* Context options.  One context drives one device (a compute stream and a copy stream). */
 typedef struct {
@@ -218,10 +227,24 @@ knn_status knn_comm_create(knn_ctx* ctx, const void* id, int32_t nranks, int32_t
 void knn_comm_destroy(knn_comm* comm);
 /* the number of ranks the RCCL communicator spans (ncclCommCount) */
 knn_status knn_comm_count(const knn_comm* comm, int32_t* nranks);
+/* *broken = 1 once a collective on this communicator failed and it was aborted: every later
+ * knn_predict_train_sharded on it returns KNN_ERCCL at once (no shard pass, no collective), so
+ * a caller that sees KNN_ERCCL can tell "a peer's shard failed, the communicator is fine" (0)
+ * from "tear down every rank and build a new communicator" (1). */
+knn_status knn_comm_broken(const knn_comm* comm, int32_t* broken);
 knn_status knn_predict_train_sharded(knn_ctx* ctx, knn_comm* comm, const knn_dataset* train_shard, int64_t idx_base,
                                      const knn_dataset* test, int32_t k, int32_t num_classes, int32_t* d_pred,
                                      float* d_dist, int32_t* d_idx, void* hip_stream);
 knn_status knn_shard_range(int64_t n, int32_t world, int32_t rank, int64_t* begin, int64_t* end);
+/* The partition of a `world`-GPU run (north_star "Partitioning"; the reference only splits the
+ * test set, multi-thread.cpp:154-158 / mpi.cpp:141-170): *policy = KNN_SHARD_TEST (queries split
+ * by knn_shard_range, train replicated, no collective on the data path) while one copy of train
+ * and its bf16 filter operands fits half of `hbm_bytes` (<= 0: 288 GiB), else KNN_SHARD_TRAIN
+ * (knn_predict_train_sharded).  The C++ KNN() (KNN_AMD_SHARD=auto), knn_cli --shard=auto and
+ * bench.py --shard auto ask it; every caller may force either partition. */
+typedef enum { KNN_SHARD_TEST = 0, KNN_SHARD_TRAIN = 1 } knn_shard_kind;
+knn_status knn_shard_policy(int64_t n_train, int64_t n_query, int32_t d, int32_t dtype, int32_t world,
+                            int64_t hbm_bytes, int32_t* policy);
 knn_status knn_exchange_layout(int64_t nq, int32_t k, int32_t world, int32_t rank, int64_t* send_off,
                                int64_t* send_cnt, int64_t* recv_off, int64_t* recv_cnt);
 

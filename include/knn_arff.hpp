@@ -174,7 +174,10 @@ int* computeConfusionMatrix(int* predictions, ArffData* dataset);
 // main.cpp:102
 float computeAccuracy(int* confusionMatrix, ArffData* dataset);
 
-// Number of GPUs KNN() shards over (env KNN_AMD_DEVICES, default: all visible).
+// Number of GPUs KNN() shards over (env KNN_AMD_DEVICES, default: all visible).  The
+// partition over them: env KNN_AMD_SHARD = test (default, the reference's split of the test
+// set, train replicated), train (train rows split by the same rule, per-shard exact top-k
+// merged on device 0 by (distance, global index)) or auto (knn_shard_policy).
 int knn_amd_num_devices();
 // Create the device contexts up front (the CLI does this before its timed region,
 // as the reference parses and MPI_Init()s before starting its clock).

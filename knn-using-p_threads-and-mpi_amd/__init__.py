@@ -21,6 +21,7 @@ visible, calls raise ``KnnError``.
 """
 import ctypes
 import os
+import weakref
 
 import numpy as np
 
@@ -44,6 +45,19 @@ class KnnError(RuntimeError):
 
 
 KNN_OPT_CACHE_TRAIN = 1
+KNN_OPT_CACHE_TRAIN_DEVICE = 2
+# contexts holding a cached device train tensor: Context.generate invalidates every one whose
+# tensor shares bytes with what it writes (a slice, a view, another context's call)
+_caching_contexts = weakref.WeakSet()
+
+
+def _byte_span(t):
+    """[first, last) device byte addresses a strided tensor covers (empty: (p, p))."""
+    p = t.data_ptr()
+    if t.numel() == 0:
+        return p, p
+    hi = sum((n - 1) * st for n, st in zip(t.shape, t.stride())) + 1
+    return p, p + hi * t.element_size()
 
 
 class knn_opts(ctypes.Structure):
@@ -98,8 +112,10 @@ def load_library(path=LIB_PATH):
         "knn_comm_create": (I32, [P, P, I32, I32, ctypes.POINTER(P)]),
         "knn_comm_destroy": (None, [P]),
         "knn_comm_count": (I32, [P, ctypes.POINTER(I32)]),
+        "knn_comm_broken": (I32, [P, ctypes.POINTER(I32)]),
         "knn_predict_train_sharded": (I32, [P, P, DS, I64, DS, I32, I32, P, P, P, P]),
         "knn_shard_range": (I32, [I64, I32, I32, ctypes.POINTER(I64), ctypes.POINTER(I64)]),
+        "knn_shard_policy": (I32, [I64, I64, I32, I32, I32, I64, ctypes.POINTER(I32)]),
         "knn_exchange_layout": (I32, [I64, I32, I32, I32, P, P, P, P]),
         "knn_alloc_pinned": (I32, [ctypes.c_size_t, ctypes.POINTER(P)]),
         "knn_free_pinned": (None, [P]),
@@ -295,8 +311,10 @@ class Context:
         # profile: False/0 off, True/1 per-stage HIP events, 2 = also count filter candidates,
         # 3 = events around the dominant stages only (filter, rescore, ...: knn_amd.h)
         # cache_train: predict() keeps the device copy of train across calls (KNN_OPT_CACHE_TRAIN)
+        # and the device calls keep the operands derived from the caller's train tensor
+        # (KNN_OPT_CACHE_TRAIN_DEVICE): this wrapper bumps the generation on every write it can see
         opts = knn_opts(device, ALGOS[algo], train_splits, int(profile),
-                        KNN_OPT_CACHE_TRAIN if cache_train else 0)
+                        KNN_OPT_CACHE_TRAIN | KNN_OPT_CACHE_TRAIN_DEVICE if cache_train else 0)
         self.cache_train = bool(cache_train)
         # the arrays whose addresses key the library's train cache (knn_predict): held until
         # the next call replaces them, so no later array can be allocated at a cached address
@@ -365,6 +383,15 @@ class Context:
         if self._dev_train is None or self._dev_train[0] is not train or self._dev_train[1] != key:
             self.set_generation(self._generation + 1)
             self._dev_train = (train, key)
+            _caching_contexts.add(self)
+
+    def _invalidate_overlap(self, span):
+        """The cached train tensor shares bytes with [span): the next device call bumps the
+        generation (the write did not go through torch, so its version counter did not move)."""
+        if self._dev_train is not None:
+            a, b = _byte_span(self._dev_train[0])
+            if a < span[1] and span[0] < b:
+                self._dev_train = None
 
     def predict_device(self, train, labels, test, k, num_classes, pred, dist=None, idx=None,
                        stream=None, d=None):
@@ -420,8 +447,12 @@ class Context:
             self.h, feat.data_ptr(), None if labels is None else labels.data_ptr(), row0,
             feat.shape[0], d, feat.shape[1], dtype, kind, seed, stream_id, num_classes,
             self._stream(stream, feat)))
-        if self._dev_train is not None and self._dev_train[0] is feat:
-            self._dev_train = None  # written behind torch's back: the next call bumps the generation
+        # written behind torch's back: every context caching a train tensor that shares bytes with
+        # feat (feat itself, a slice or view of it, a tensor feat is a view of) bumps its
+        # generation at its next call
+        span = _byte_span(feat)
+        for c in list(_caching_contexts):
+            c._invalidate_overlap(span)
 
     def confusion_matrix_device(self, pred, labels, num_classes, cm=None, stream=None):
         """computeConfusionMatrix / computeAccuracy (main.cpp:87-112) on device tensors:
@@ -504,6 +535,18 @@ def shard_range_c(n, world, rank):
     return a.value, b.value
 
 
+def shard_policy(n_train, n_query, d, dtype, world, hbm_bytes=0):
+    """knn_shard_policy: "test" (queries split, train replicated) or "train" (train split,
+    per-shard top-k exchanged and merged) for a world-GPU run.  dtype: "f32" or "bf16"."""
+    lib = load_library()
+    p = ctypes.c_int32()
+    st = lib.knn_shard_policy(n_train, n_query, d, KNN_BF16 if dtype == "bf16" else KNN_F32, world, hbm_bytes,
+                              ctypes.byref(p))
+    if st != KNN_OK:
+        raise KnnError(st, "knn_shard_policy")
+    return "train" if p.value == 1 else "test"
+
+
 def exchange_layout(nq, k, world, rank):
     """knn_exchange_layout: (send_off, send_cnt, recv_off, recv_cnt) int32-element arrays of
     the train-sharded all-to-all of rank `rank`."""
@@ -554,6 +597,14 @@ class Comm:
         if st != KNN_OK:
             raise KnnError(st, "knn_comm_count")
         return n.value
+
+    def broken(self):
+        """True once a collective failed and the communicator was aborted (knn_comm_broken)."""
+        b = ctypes.c_int32()
+        st = self.lib.knn_comm_broken(self.h, ctypes.byref(b))
+        if st != KNN_OK:
+            raise KnnError(st, "knn_comm_broken")
+        return bool(b.value)
 
     def close(self):
         if getattr(self, "h", None):

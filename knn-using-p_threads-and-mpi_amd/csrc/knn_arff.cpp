@@ -32,6 +32,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -345,6 +347,8 @@ uint64_t knn_flat_view_uid() {
     return next.fetch_add(1, std::memory_order_relaxed);
 }
 
+int knn_ctx_device(const knn_ctx* c);  // (knn_capi.cpp: the device a context drives)
+
 namespace {
 
 // Flatten features [0, na-1) and the class attribute with operator float semantics.
@@ -389,8 +393,10 @@ std::vector<knn_ctx*>& contexts() {
     std::lock_guard<std::mutex> g(D.mu);
     if (D.ctx.empty()) {
         int n = knn_amd_num_devices();
+        int phys = 0;
+        if (hipGetDeviceCount(&phys) != hipSuccess || phys < 1) phys = 1;
         for (int i = 0; i < n; i++) {
-            knn_opts o{i, KNN_ALGO_AUTO, 0, 0, KNN_OPT_CACHE_TRAIN};  // ArffData is immutable once parsed
+            knn_opts o{i % phys, KNN_ALGO_AUTO, 0, 0, KNN_OPT_CACHE_TRAIN};  // ArffData is immutable once parsed
             knn_ctx* c = nullptr;
             knn_status s = knn_create(&c, &o);
             if (s != KNN_OK) {
@@ -402,6 +408,90 @@ std::vector<knn_ctx*>& contexts() {
         }
     }
     return D.ctx;
+}
+
+// The partition KNN() uses over G devices: KNN_AMD_SHARD = test (default: the reference's rule,
+// queries split, train replicated), train (train rows split, per-shard top-k merged) or auto
+// (knn_shard_policy: train-sharded when one copy of train does not fit a device)
+int shard_mode(int64_t nt, int64_t nq, int d, int G) {
+    const char* e = std::getenv("KNN_AMD_SHARD");
+    if (G <= 1 || !e || !std::strcmp(e, "test")) return KNN_SHARD_TEST;
+    if (!std::strcmp(e, "train")) return KNN_SHARD_TRAIN;
+    if (std::strcmp(e, "auto")) throwf("KNN: KNN_AMD_SHARD=%s (test, train or auto)", e);
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) tot = 0;
+    int32_t p = KNN_SHARD_TEST;
+    if (knn_shard_policy(nt, nq, d, KNN_F32, G, (int64_t)tot, &p) != KNN_OK) p = KNN_SHARD_TEST;
+    return p;
+}
+
+// device buffer of one call (freed on every exit path)
+struct DevMem {
+    void* p = nullptr;
+    int dev = 0;
+    DevMem(int device, size_t bytes) : dev(device) {
+        if (hipSetDevice(dev) != hipSuccess || hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) p = nullptr;
+    }
+    ~DevMem() {
+        if (p) { (void)hipSetDevice(dev); (void)hipFree(p); }
+    }
+    DevMem(const DevMem&) = delete;
+    DevMem& operator=(const DevMem&) = delete;
+};
+
+// Train-sharded KNN() over G devices (the reference only splits the test set):
+// device g holds train rows shard_range(n, G, g) and the queries [q0, q1), and computes its
+// shard's exact top-k of every query as (distance bits, global index, label) records
+// (knn_shard_topk_device); device 0 gathers the G record blocks and merges them by (distance,
+// global index) -- the reference's lower-index tie rule over the whole train set -- and votes
+// (knn_merge_vote_device).  Bit-identical to the test-sharded result.
+void predict_range_train_sharded(const KnnFlatView& tr, const KnnFlatView& te, int k, int C, int64_t q0, int64_t q1,
+                                 int* out, std::vector<knn_ctx*>& cs, int G) {
+    const int64_t nq = q1 - q0;
+    const size_t recb = sizeof(int32_t) * 3 * (size_t)k * (size_t)nq;
+    std::vector<std::unique_ptr<DevMem>> rec(G);
+    std::vector<knn_status> st(G, KNN_OK);
+    std::vector<std::string> why(G);
+    std::vector<std::thread> th;
+    for (int g = 0; g < G; g++) {
+        auto job = [&, g]() {
+            std::lock_guard<std::mutex> busy(*devices().busy[g]);
+            int64_t t0 = 0, t1 = 0;
+            knn_shard_range(tr.n, G, g, &t0, &t1);
+            const size_t tb = sizeof(float) * (size_t)tr.ld * (size_t)(t1 - t0), qb = sizeof(float) * (size_t)te.ld * (size_t)nq;
+            const int dev = knn_ctx_device(cs[g]);
+            DevMem dt(dev, tb), dl(dev, sizeof(int32_t) * (size_t)(t1 - t0)), dq(dev, qb);
+            rec[g].reset(new DevMem(dev, recb));
+            if (!dt.p || !dl.p || !dq.p || !rec[g]->p) { st[g] = KNN_ENOMEM; why[g] = "device allocation"; return; }
+            if (hipMemcpy(dt.p, tr.feat.data() + (size_t)t0 * tr.ld, tb, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(dl.p, tr.labels.data() + t0, sizeof(int32_t) * (size_t)(t1 - t0), hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(dq.p, te.feat.data() + (size_t)q0 * te.ld, qb, hipMemcpyHostToDevice) != hipSuccess) {
+                st[g] = KNN_EHIP; why[g] = "upload"; return;
+            }
+            knn_dataset dtr{dt.p, (const int32_t*)dl.p, t1 - t0, tr.d, tr.ld, KNN_F32};
+            knn_dataset dte{dq.p, nullptr, nq, te.d, te.ld, KNN_F32};
+            st[g] = knn_shard_topk_device(cs[g], &dtr, &dte, k, C, t0, (int32_t*)rec[g]->p, nullptr);
+            if (st[g] != KNN_OK) why[g] = knn_last_error(cs[g]);
+        };
+        th.emplace_back(job);
+    }
+    for (auto& t : th) t.join();
+    for (int g = 0; g < G; g++)
+        if (st[g] != KNN_OK) throwf("KNN (train-sharded, device %d): %s (status %d)", g, why[g].c_str(), (int)st[g]);
+    // the exchange: every shard's records to device 0, [G][nq][3][k]
+    std::lock_guard<std::mutex> busy(*devices().busy[0]);
+    const int dev0 = knn_ctx_device(cs[0]);
+    DevMem all(dev0, recb * (size_t)G), pred(dev0, sizeof(int32_t) * (size_t)nq);
+    if (!all.p || !pred.p) throwf("KNN (train-sharded): device allocation failed");
+    for (int g = 0; g < G; g++)
+        if (hipMemcpyPeer((char*)all.p + recb * (size_t)g, dev0, rec[g]->p, rec[g]->dev, recb) != hipSuccess)
+            throwf("KNN (train-sharded): copy of shard %d's lists failed", g);
+    (void)hipSetDevice(dev0);
+    const knn_status s = knn_merge_vote_device(cs[0], G, nq, k, C, (const int32_t*)all.p, (int32_t*)pred.p, nullptr,
+                                               nullptr, nullptr);
+    if (s != KNN_OK) throwf("KNN (train-sharded merge): %s (status %d)", knn_last_error(cs[0]), (int)s);
+    if (hipMemcpy(out, pred.p, sizeof(int32_t) * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess)
+        throwf("KNN (train-sharded): download failed");
 }
 
 // predictions for test rows [q0, q1), sharded over the devices by the reference rule
@@ -420,6 +510,8 @@ void predict_range(ArffData* train, ArffData* test, int k, int64_t q0, int64_t q
     knn_dataset dtr{tr.feat.data(), tr.labels.data(), tr.n, tr.d, tr.ld, KNN_F32};
     knn_dataset dte{te.feat.data(), nullptr, te.n, te.d, te.ld, KNN_F32};
     std::vector<knn_ctx*>& cs = contexts();
+    if (cs.size() > 1 && shard_mode(tr.n, nq, tr.d, (int)std::min<int64_t>((int64_t)cs.size(), tr.n)) == KNN_SHARD_TRAIN)
+        return predict_range_train_sharded(tr, te, k, C, q0, q1, out, cs, (int)std::min<int64_t>((int64_t)cs.size(), tr.n));
     const int G = (int)std::min<int64_t>((int64_t)cs.size(), nq);
     std::vector<knn_status> st(G, KNN_OK);
     std::vector<std::thread> th;
@@ -637,6 +729,10 @@ int knn_amd_num_devices() {
     if (const char* e = std::getenv("KNN_AMD_DEVICES")) {
         int want = std::atoi(e);
         if (want > 0 && want < n) n = want;
+        // KNN_AMD_SHARE_GPU=1: more workers than GPUs, worker w on GPU w % n (rehearses an
+        // N-GPU partition, the train-sharded exchange included, on fewer devices)
+        const char* sh = std::getenv("KNN_AMD_SHARE_GPU");
+        if (want > n && n > 0 && sh && !std::strcmp(sh, "1")) n = std::min(want, 64);
     }
     return n;
 }

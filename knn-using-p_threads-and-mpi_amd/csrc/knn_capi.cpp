@@ -78,6 +78,14 @@ struct knn_ctx {
     struct { const void* feat; int64_t n; int d, ld, dtype; uint64_t gen, epoch; bool valid; }
         tpad{nullptr, 0, 0, 0, 0, 0, 0, false};
     int rescore_su = 0;  // test hook KNN_RESCORE_SU: the rescore's LDS staging size (0 = sized)
+    // study overrides of the fused filter's plan (KNN_FUSED_QG / _NBUF / _HEAPS), read once at
+    // knn_create: a call never reads the environment, and one pass uses one plan throughout
+    FusedForce fforce;
+    // the device entry points reuse derived train operands across calls only under
+    // KNN_OPT_CACHE_TRAIN_DEVICE (the caller's device buffer may change behind the library)
+    int cache_train_device = 0;
+    // study switches of run_gemm, read once at knn_create
+    bool no_lshare = false, no_cursor = false, rescore_all = false;
     // host-API staging (device copies of host inputs / outputs)
     DBuf h_train, h_labels, h_test, h_pred, h_dist, h_idx;
     int32_t* ctrl_host = nullptr;  // pinned: [0] status, [1] fallback count
@@ -383,7 +391,7 @@ int max_splits(int64_t nt, int k, int cap) {
 }
 
 int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int rb, int k, int cap,
-                  bool fused = false, int d = 0, int64_t nq = 0) {
+                  bool fused = false, int d = 0, const FilterPlan* fplan = nullptr) {
     if (c->train_splits > 0) return std::min(8, c->train_splits);
     // More segments shrink the partial last wave of blocks (measured on config A:
     // S=3 224 ms, S=5 217 ms, S=8 216 ms), but each segment must fit its rows in its
@@ -392,7 +400,7 @@ int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int
     // tile; the slice gets a 1.5x margin.  Overflowing queries still finish exactly,
     // on the slow full-scan fallback.
     int occ = 1;
-    const hipError_t oe = fused ? knn_fused_occupancy(d, k, &occ, nq, c->num_cus) : knn_gemm_filter_occupancy(dtype, rb, k, &occ);
+    const hipError_t oe = fused ? knn_fused_occupancy(d, *fplan, &occ) : knn_gemm_filter_occupancy(dtype, rb, k, &occ);
     if (oe != hipSuccess || occ < 1) occ = 1;
     const int64_t slots = (int64_t)occ * c->num_cus;
     int best = 1;
@@ -433,8 +441,10 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     HIP_OR_FAIL(c, c->fb_list.ensure(sizeof(int32_t) * nq));
 
     // bf16 MFMA operands (rounded fp32 rows or bf16 data) run the fused-norm filter
-    const bool fused = (felem == ELEM_ROUND || felem == ELEM_BF16) && knn_fused_supported(d) &&
-                       knn_fused_plan(d, k, nq, c->num_cus).nw > 0;
+    // the fused filter's plan, computed once: it sizes the tile blocks (bn_f), the occupancy,
+    // the schedule and the launch of this pass
+    const FilterPlan fplan = knn_fused_supported(d) ? knn_fused_plan(d, k, nq, c->num_cus, c->fforce) : FilterPlan{};
+    const bool fused = (felem == ELEM_ROUND || felem == ELEM_BF16) && knn_fused_supported(d) && fplan.nw > 0;
     float coef, eta;
     if (fused) {
         certificate_fused(d, felem == ELEM_ROUND, &coef, &eta);
@@ -448,10 +458,13 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     // context caches train (no train pass at all then; main.cpp:40-43 re-reads every train row
     // per query, this is the part of that work that depends on train alone)
     const bool fused_tn = fused && knn_fused_row_bytes(d) == 2 * d;
-    const int bn_f = fused ? 32 * knn_fused_plan(d, k, nq, c->num_cus).rg : 0;
+    const int bn_f = fused ? 32 * fplan.rg : 0;
     const bool own_train = tr->feat == c->h_train.p;  // knn_predict's uploaded copy
+    // derived train operands are reused for knn_predict's own upload (KNN_OPT_CACHE_TRAIN), and
+    // for a caller's device buffer only under KNN_OPT_CACHE_TRAIN_DEVICE
+    const bool may_cache = c->cache_train && (own_train || c->cache_train_device);
     auto& tp = c->tprep;
-    const bool prep_hit = fused_tn && !gate && c->cache_train && tp.valid && tp.feat == tr->feat && tp.n == nt &&
+    const bool prep_hit = fused_tn && !gate && may_cache && tp.valid && tp.feat == tr->feat && tp.n == nt &&
                           tp.d == d && tp.ld == tr->ld && tp.dtype == dtype && tp.bn == bn_f &&
                           tp.gen == c->generation && tp.epoch == (own_train ? c->train_epoch : 0);
     if (fused_tn && !gate) {
@@ -512,7 +525,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         ftrain = c->tblk.p; ftest = c->split_q.p;
         fld_t = fld_q = d;
         c->stats[8] = prep_hit ? 1 : 0;
-        if (c->cache_train)
+        if (may_cache)
             tp = {tr->feat, nt, d, tr->ld, dtype, bn_f, c->generation, own_train ? c->train_epoch : 0, true};
     } else if (fused) {
         // (study build KNN_STUDY_AUG64, d = 64) augmented bf16 rows: train [rn(t) | tn split],
@@ -557,7 +570,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         const size_t es = (size_t)elem_size(dtype), pitch = es * (size_t)tr->ld;
         auto& pk = c->tpad;
         const uint64_t ep = tr->feat == c->h_train.p ? c->train_epoch : 0;
-        const bool hit = c->cache_train && pk.valid && pk.feat == tr->feat && pk.n == nt && pk.d == d &&
+        const bool hit = may_cache && pk.valid && pk.feat == tr->feat && pk.n == nt && pk.d == d &&
                          pk.ld == tr->ld && pk.dtype == dtype && pk.gen == c->generation && pk.epoch == ep;
         pk.valid = false;
         if (!hit) {
@@ -565,13 +578,12 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
             HIP_OR_FAIL(c, hipMemcpyAsync(c->pad_t.p, tr->feat, pitch * (size_t)nt, hipMemcpyDeviceToDevice, st));
             HIP_OR_FAIL(c, hipMemsetAsync((unsigned char*)c->pad_t.p + pitch * (size_t)nt, 0, pitch * (size_t)(ntp - nt), st));
         }
-        if (c->cache_train) pk = {tr->feat, nt, d, tr->ld, dtype, c->generation, ep, true};
+        if (may_cache) pk = {tr->feat, nt, d, tr->ld, dtype, c->generation, ep, true};
         ftrain = c->pad_t.p;
     }
 
-    const FilterPlan plan = fused ? knn_fused_plan(d, k, nq, c->num_cus) : knn_gemm_filter_plan(kelem, rb, k);
-    static const bool no_lshare = getenv("KNN_NO_LIST_SHARE") != nullptr;
-    const bool shared = fused && !no_lshare && knn_fused_list_share_width(plan) > 0;
+    const FilterPlan plan = fused ? fplan : knn_gemm_filter_plan(kelem, rb, k);
+    const bool shared = fused && !c->no_lshare && knn_fused_list_share_width(plan) > 0;
     const int64_t n_qtiles = (nq + plan.bm - 1) / plan.bm;
     GemmFilterArgs g{};
     g.nt = nt; g.n_qtiles = (int)n_qtiles;
@@ -580,13 +592,13 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     int nseg = 0;
     if (fused && c->train_splits <= 0) {
         int occ = 1;
-        if (knn_fused_occupancy(d, k, &occ, nq, c->num_cus) != hipSuccess || occ < 1) occ = 1;
+        if (knn_fused_occupancy(d, plan, &occ) != hipSuccess || occ < 1) occ = 1;
         int nb = 1;
         knn_fused_schedule(g, occ * c->num_cus, &nb);
         if (nb <= max_splits(nt, k, cap)) nseg = nb;
     }
     if (nseg == 0) {
-        nseg = choose_splits(c, n_qtiles, nt, kelem, rb, k, cap, fused, d, nq);
+        nseg = choose_splits(c, n_qtiles, nt, kelem, rb, k, cap, fused, d, &plan);
         g.g2 = -1;  // segment schedule
     }
     int64_t seg_len = (nt + nseg - 1) / nseg;
@@ -603,8 +615,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     // per-XCD scan cursors for the multi-segment schedule (B: filter traffic beyond L2 664 ->
     // 494 GB per launch, time unchanged; with one segment or the balanced schedule they saved
     // nothing: r03s).  KNN_NO_SCAN_CURSOR=1 turns them off (a diagnostic; same results).
-    static const bool no_cursor = getenv("KNN_NO_SCAN_CURSOR") != nullptr;
-    if (fused && !no_cursor && g.g2 < 0 && nseg > 1) {
+    if (fused && !c->no_cursor && g.g2 < 0 && nseg > 1) {
         HIP_OR_FAIL(c, c->cursor.ensure(sizeof(uint32_t) * 8));
         HIP_OR_FAIL(c, hipMemsetAsync(c->cursor.p, 0, sizeof(uint32_t) * 8, st));
         g.cursor = c->cursor.as<uint32_t>();
@@ -640,8 +651,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     r.gate = gate;
     // the fused filter's final thresholds: the selection stages only the candidates that can
     // survive (KNN_RESCORE_ALL=1 stages every candidate: a study switch)
-    static const bool rescore_all = getenv("KNN_RESCORE_ALL") != nullptr;
-    r.gthr = fused && !rescore_all ? g.gthr : nullptr;
+    r.gthr = fused && !c->rescore_all ? g.gthr : nullptr;
     // LDS staging for about twice the expected kept rows -- k (1 + ln(nt / k)) for one scan,
     // +25 % per extra segment (they share thresholds through gthr), measured 238 per query on
     // A and 605 on B -- rounded to 64 by the launcher and capped at the list capacity: a
@@ -685,9 +695,16 @@ knn_status knn_create(knn_ctx** out, const knn_opts* opts) {
         c->train_splits = opts->train_splits;
         c->profile = opts->profile;
         c->cache_train = (opts->flags & KNN_OPT_CACHE_TRAIN) != 0;
+        c->cache_train_device = c->cache_train && (opts->flags & KNN_OPT_CACHE_TRAIN_DEVICE) != 0;
     }
-    // test hook: the rescore's LDS staging size (read here once, never per call)
+    // test hooks and study switches, read here once, never per call
     if (const char* e = getenv("KNN_RESCORE_SU")) c->rescore_su = atoi(e);
+    if (const char* e = getenv("KNN_FUSED_QG")) c->fforce.qg = atoi(e);
+    if (const char* e = getenv("KNN_FUSED_NBUF")) c->fforce.nbuf = atoi(e);
+    c->fforce.heaps = getenv("KNN_FUSED_HEAPS") != nullptr;
+    c->no_lshare = getenv("KNN_NO_LIST_SHARE") != nullptr;
+    c->no_cursor = getenv("KNN_NO_SCAN_CURSOR") != nullptr;
+    c->rescore_all = getenv("KNN_RESCORE_ALL") != nullptr;
     if (c->device < 0 || c->device >= ndev) { delete c; return KNN_ENODEV; }
     hipDeviceProp_t prop;
     if (hipSetDevice(c->device) != hipSuccess || hipGetDeviceProperties(&prop, c->device) != hipSuccess) {

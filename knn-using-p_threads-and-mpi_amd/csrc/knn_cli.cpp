@@ -1,15 +1,17 @@
 // knn_cli.cpp -- command-line driver with the reference's contract.
 //
-//   knn_cli train.arff test.arff k [numDevices]
+//   knn_cli train.arff test.arff k [numDevices] [--shard=test|train|auto]
 //
 // Same positional arguments as ./main (main.cpp:114-122; k parsed with strtol) plus the
 // optional worker count of ./multi-thread (multi-thread.cpp:135-143), here the number of
-// GPUs the test set is sharded over.  The timed region is the reference's: the KNN()
+// GPUs the work is split over: the test set by the reference's rule (default), or
+// --shard=train the train set (per-shard top-k merged), --shard=auto knn_shard_policy.  The timed region is the reference's: the KNN()
 // call only (main.cpp:133-137), after parsing and device initialisation.  The report
 // line is printed verbatim (main.cpp:146), "CPU time" wording included.
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <ctime>
 #include <iostream>
 #include <string>
@@ -17,8 +19,16 @@
 #include "../../include/knn_arff.hpp"
 
 int main(int argc, char* argv[]) {
+    // --shard=... may sit anywhere; the rest are the reference's positional arguments
+    int n = 0;
+    for (int i = 0; i < argc; i++) {
+        if (!std::strncmp(argv[i], "--shard=", 8)) setenv("KNN_AMD_SHARD", argv[i] + 8, 1);
+        else argv[n++] = argv[i];
+    }
+    argc = n;
     if (argc != 4 && argc != 5) {
-        std::cout << "Usage: ./knn_cli datasets/train.arff datasets/test.arff k [numDevices]" << std::endl;
+        std::cout << "Usage: ./knn_cli datasets/train.arff datasets/test.arff k [numDevices] [--shard=test|train|auto]"
+                  << std::endl;
         std::exit(0);
     }
     int k = (int)std::strtol(argv[3], NULL, 10);

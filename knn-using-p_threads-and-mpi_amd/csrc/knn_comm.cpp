@@ -135,6 +135,21 @@ knn_status knn_shard_range(int64_t n, int32_t world, int32_t rank, int64_t* begi
     return KNN_OK;
 }
 
+knn_status knn_shard_policy(int64_t n_train, int64_t n_query, int32_t d, int32_t dtype, int32_t world,
+                            int64_t hbm_bytes, int32_t* policy) {
+    if (n_train < 0 || n_query < 0 || d < 1 || world < 1 || !policy || (dtype != KNN_F32 && dtype != KNN_BF16))
+        return KNN_EINVAL;
+    // north_star's rule: replicate train (test-sharded, no collective on the data path) while a
+    // full copy fits one GPU's HBM with room for the filter's derived operands (bf16 tile blocks:
+    // half an fp32 copy; one bf16 copy) and the per-query workspace (candidate lists, 24 KB per
+    // query of a pass, bounded separately); else shard train and exchange per-shard top-k lists
+    const double esz = dtype == KNN_BF16 ? 2.0 : 4.0;
+    const double train_b = (double)n_train * d * esz + (double)n_train * d * 2.0;
+    const double budget = 0.5 * (double)(hbm_bytes > 0 ? hbm_bytes : (int64_t)288 << 30);
+    *policy = (world > 1 && train_b > budget) ? KNN_SHARD_TRAIN : KNN_SHARD_TEST;
+    return KNN_OK;
+}
+
 knn_status knn_exchange_layout(int64_t nq, int32_t k, int32_t world, int32_t rank, int64_t* send_off,
                                int64_t* send_cnt, int64_t* recv_off, int64_t* recv_cnt) {
     if (nq < 0 || k < 1 || world < 1 || rank < 0 || rank >= world || !send_off || !send_cnt || !recv_off || !recv_cnt)
@@ -207,6 +222,12 @@ knn_status knn_comm_count(const knn_comm* c, int32_t* nranks) {
     return KNN_OK;
 }
 
+knn_status knn_comm_broken(const knn_comm* c, int32_t* broken) {
+    if (!c || !broken) return KNN_EINVAL;
+    *broken = c->broken ? 1 : 0;
+    return KNN_OK;
+}
+
 void knn_comm_destroy(knn_comm* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
@@ -231,6 +252,9 @@ knn_status knn_predict_train_sharded(knn_ctx* ctx, knn_comm* comm, const knn_dat
     const int64_t nq = test->n;
     int64_t m0, m1;
     knn_shard_range(nq, comm->nranks, comm->rank, &m0, &m1);
+    // an aborted communicator (an earlier collective failed) can reach no peer: fail at once,
+    // before paying for a shard pass (knn_comm_broken lets the caller tear every rank down)
+    if (comm->broken) return KNN_ERCCL;
     if (hipSetDevice(comm->device) != hipSuccess) return KNN_EHIP;
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : (hipStream_t)knn_ctx_stream(ctx);
     const size_t row = 3 * (size_t)k * sizeof(int32_t);
@@ -258,7 +282,6 @@ knn_status knn_predict_train_sharded(knn_ctx* ctx, knn_comm* comm, const knn_dat
         comm->broken = true;
         return KNN_ERCCL;
     };
-    if (comm->broken) return KNN_ERCCL;
     const int32_t* vote_src = comm->flag + (s == KNN_OK ? 1 : 2);
     if (r.all_reduce(vote_src, comm->flag, 1, ncclInt32, ncclMax, comm->comm, st) != ncclSuccess) return give_up();
     if (hipMemcpyAsync(comm->flag_host, comm->flag, sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||

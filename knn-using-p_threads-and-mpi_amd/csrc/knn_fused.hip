@@ -1166,15 +1166,14 @@ int knn_fused_row_bytes(int d) { return d == 64 && KNN_FUSED_AUG64 ? 2 * d + 32 
 //    8-wave blocks: pairs when they fit beside the heaps, else two buffers, else 32-row tiles.
 // Register lists: k <= 16 keeps per-query lists (KR = 16), k <= 32 per-half lists (KR = 32,
 // 16 entries: exact 32-entry lists cost a block per CU of occupancy and 9 % of time on B).
-FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus) {
+FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus, const FusedForce& force) {
     const int rb = knn_fused_row_bytes(d);
     const size_t cap = 160 * 1024 - 256;  // room for the kernel's static LDS
     // d = 256, 32 < k <= 104 (C): per-half 52-entry register lists instead of LDS heaps, so
     // the tile buffers get the LDS the heaps held -- 32-row tiles in quads (one barrier per 128
-    // rows) instead of one barrier per 32-row tile (KNN_FUSED_HEAPS=1: the heap shape).  (64-row
+    // rows) instead of one barrier per 32-row tile (force.heaps: the heap shape).  (64-row
     // tiles in pairs, the other way to the same barrier count, spill: two more accumulators.)
-    const bool force_heaps = getenv("KNN_FUSED_HEAPS") != nullptr;
-    const int kr = k <= 16 ? 16 : k <= 32 ? 32 : (k <= 104 && d == 256 && !force_heaps) ? 104 : 0;
+    const int kr = k <= 16 ? 16 : k <= 32 ? 32 : (k <= 104 && d == 256 && !force.heaps) ? 104 : 0;
     auto make = [&](int nw, int rg, int minw, int nbuf, int qg = 1) {
         FilterPlan f{nw, qg, rg, minw, nbuf, 32 * qg * nw, fused_lds_of(rb, k, nw, rg, nbuf, kr == 0, qg)};
         f.kr = kr;
@@ -1187,19 +1186,15 @@ FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus) {
     // (each piece starts its thresholds from +inf), so they keep 32 per wave on 64-row tiles.
     // Same box (profiles/r04c): A 24.08 -> 23.19 ms, B 575.9 -> 550.9 ms; A's 8-GPU share
     // (12,500 queries) 3.40 -> 6.33 ms with QG = 2, hence the rule.
-    // KNN_FUSED_QG=1|2 forces the choice (study switch; read per call, tests flip it).
-    const char* qe = getenv("KNN_FUSED_QG");
-    const int qg_env = qe ? atoi(qe) : 0;
+    // force.qg = 1|2 forces the choice (a study override, snapshot at knn_create).
     // (d = 256 keeps 32 queries per wave: two query groups' operands alone are 128 VGPRs)
-    const bool qg2 = d <= 128 && (qg_env == 2 || (qg_env != 1 && nq >= (int64_t)384 * num_cus));
-    // (KNN_FUSED_NBUF=4 forces pairs for the register-list shapes: a study switch)
-    const char* ne = getenv("KNN_FUSED_NBUF");
+    const bool qg2 = d <= 128 && (force.qg == 2 || (force.qg != 1 && nq >= (int64_t)384 * num_cus));
     // tiles in octets: 16 buffers, one barrier per eight 32-row tiles, the loop running whole
     // groups so each tile's place is static (pairs -> quads: B 557.2 -> 501.1 ms, A 22.61 ->
     // 21.67 ms, r04i; quads -> octets: A 21.49 -> 20.80 ms, B 504.6 -> 483.8 ms, r04y).
-    // KNN_FUSED_NBUF=4|8 forces pairs or quads (a study switch).
+    // force.nbuf = 4|8 forces pairs or quads (a study override).
     if (kr > 0 && qg2) {
-        const int nb = ne && atoi(ne) == 4 ? 4 : ne && atoi(ne) == 8 ? 8 : 16;
+        const int nb = force.nbuf == 4 || force.nbuf == 8 ? force.nbuf : 16;
         return make(8, 1, 2, fused_lds_of(rb, k, 8, 1, nb, false, 2) <= cap ? nb : 8, 2);
     }
     if (kr == 104) return make(8, 1, 2, 8);
@@ -1208,8 +1203,8 @@ FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus) {
     // QG = 1's 3.38 -- more pieces, more kept rows: r04l, r04p)
     if (kr > 0) {
         // 64-row tiles in quads when eight buffers fit (d <= 128): A's 8-GPU share 3.08 -> 2.96 ms,
-        // A at QG = 1 23.05 -> 22.31 (r04u); KNN_FUSED_NBUF=4 forces pairs (a study switch)
-        const bool q8 = !(ne && atoi(ne) == 4) && fused_lds_of(rb, k, 8, 2, 8, false) <= cap;
+        // A at QG = 1 23.05 -> 22.31 (r04u); force.nbuf = 4 forces pairs (a study override)
+        const bool q8 = force.nbuf != 4 && fused_lds_of(rb, k, 8, 2, 8, false) <= cap;
         FilterPlan f = make(8, 2, 2, q8 ? 8 : 4);
         f.ls = 1;
         return f;
@@ -1258,8 +1253,7 @@ static const void* fused_ptr(int d, const FilterPlan& f) {
     return d == 128 ? fused_fn<256>(f) : fused_fn<512>(f);
 }
 
-hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu, int64_t nq, int num_cus) {
-    const FilterPlan f = knn_fused_plan(d, k, nq, num_cus);
+hipError_t knn_fused_occupancy(int d, const FilterPlan& f, int* blocks_per_cu) {
     if (!knn_fused_supported(d) || f.nw == 0) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fused_ptr(d, f), 64 * f.nw, f.lds);
 }

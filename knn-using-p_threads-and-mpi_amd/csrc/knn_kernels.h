@@ -165,11 +165,21 @@ hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st);
 // fused-norm filter (knn_fused.hip), d in {64, 128, 256}: train as tile blocks [bn rows rn(t) |
 // bn fp32 norms | tile statistics] (k_tn_rows), each accumulator starting from the norms
 bool knn_fused_supported(int d);
+// Study overrides of the fused plan (the product plan is knn_fused_plan's rule; a context
+// snapshots these once, at knn_create, from KNN_FUSED_QG / KNN_FUSED_NBUF / KNN_FUSED_HEAPS so
+// the tests can run every shape): qg 1|2 forces the queries per wave, nbuf 4|8|16 the tile
+// group, heaps the LDS-heap shape for 32 < k <= 104 at d = 256.  0 / false: the rule.
+struct FusedForce {
+    int qg = 0;
+    int nbuf = 0;
+    bool heaps = false;
+};
 // nw == 0: k too large.  nq, num_cus pick the queries per wave (register-list shapes): 64 on
 // 32-row tiles when the queries fill about 3/4 of a round of 512-query blocks, else 32 on 64-row
-// tiles (fewer pieces per query tile)
-FilterPlan knn_fused_plan(int d, int k, int64_t nq = 0, int num_cus = 256);
-hipError_t knn_fused_occupancy(int d, int k, int* blocks_per_cu, int64_t nq = 0, int num_cus = 256);
+// tiles (fewer pieces per query tile).  run_gemm computes the plan once per pass and sizes the
+// operands, the occupancy, the schedule and the launch from that one plan.
+FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus, const FusedForce& force);
+hipError_t knn_fused_occupancy(int d, const FilterPlan& f, int* blocks_per_cu);
 // whether plan f's kernel exchanges threshold lists between a query's pieces (a.lshare, lshare_w floats per piece)
 int knn_fused_list_share_width(const FilterPlan& f);
 // fills a.p1_blocks / g2 / w2 / tiles64 for the balanced schedule over `slots` resident

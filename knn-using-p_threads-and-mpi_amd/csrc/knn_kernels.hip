@@ -309,13 +309,42 @@ __global__ __launch_bounds__(256) void k_exact_scan(ExactScanArgs a) {
 //    a ballot against its running k-th distance (rows of a wave arrive in ascending
 //    order, so `D < k-th distance` is exactly main.cpp:47's strict test), and a wave
 //    bitonic merge only when some lane passes.
+//  * SH (k <= 16): the list lives in lanes 0..k-1 of T[i][0], and a tile with at most
+//    DT_SHIFT_MAX passing rows inserts them one at a time, in row order, by a lane shift
+//    (shift_insert: two DPP row_shr:1 moves and a few selects per row) instead of a 64-key
+//    bitonic sort + merge (~300 instructions).  After a segment's first tiles the threshold
+//    is tight and a tile has one or two passing rows per query at most (config L, k = 5:
+//    about 34 insertions per query over a 27-tile segment); the sort remains for the dense
+//    first tiles.
 //  * Segments: blockIdx = seg * n_qblocks + qb (co-resident blocks stream the same
 //    rows).  With nseg > 1 each block writes its segment's exact top-k as records
 //    (dist bits, local row, label) [nseg][nq][3][k], merged by k_merge_vote.
 // LDS: 2 tile buffers [64][stride] f32 | per-wave class counts [8][Cpad] (vote_lds)
 // ---------------------------------------------------------------------------------
+// Insert key y into the ascending list held in lanes 0..15 of T (lanes >= k hold KEY_NONE and
+// are left alone: in_list = lane < k).  y's train index is above every listed one (rows are
+// visited in ascending order), so `T > y` on the 64-bit keys is main.cpp:47's strict `<` on the
+// distance.  Lane e takes lane e-1's key (row_shr:1; lane 0 of a row reads 0 <= y) when both
+// are above y, y itself when only its own is: the first key above y moves up one lane and the
+// k-th falls off.  Needs k <= 16 (one DPP row).
+__device__ __forceinline__ void shift_insert(u64& T, u64 y, bool in_list) {
+    const uint32_t phi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(T >> 32), 0x111, 0xF, 0xF, true);
+    const uint32_t plo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)T, 0x111, 0xF, 0xF, true);
+    const u64 prev = ((u64)phi << 32) | (u64)plo;
+    const bool gt = in_list && T > y;
+    T = gt ? (prev > y ? prev : y) : T;
+}
+// distance of list element k-1 (wave-uniform): the insertion threshold, FLT_MAX while the list
+// has fewer than k keys (main.cpp:33's sentinel)
+__device__ __forceinline__ float kth_dist(u64 T, int k) {
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(T >> 32), k - 1);
+    return hi == 0xffffffffu ? FLT_MAX : __uint_as_float(hi);
+}
+#ifndef DT_SHIFT_MAX
+#define DT_SHIFT_MAX 8  // passing rows per tile and query up to which the lane shift beats the sort
+#endif
 #pragma clang fp contract(off)
-template <int QW, int R, typename E>
+template <int QW, int R, typename E, bool SH>
 __global__ __launch_bounds__(64 * DT_NW, 4) void k_direct_tile(DirectTileArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NT = 64 * DT_NW;
@@ -427,10 +456,31 @@ __global__ __launch_bounds__(64 * DT_NW, 4) void k_direct_tile(DirectTileArgs a)
 #pragma unroll
             for (int i = 0; i < QW; i++) {
                 const bool pass = valid && acc[i] < thr[i];
-                if (__ballot(pass)) {
-                    topk_merge<R>(T[i], pass ? make_key(acc[i], (uint32_t)row) : KEY_NONE);
-                    const u64 kth = list_at(T[i], k - 1);
-                    thr[i] = kth == KEY_NONE ? FLT_MAX : __uint_as_float((uint32_t)(kth >> 32));
+                u64 m = __ballot(pass);
+                if (m) {
+                    if (SH && __popcll(m) <= DT_SHIFT_MAX) {
+                        // one row at a time, ascending: each re-tested against the threshold
+                        // the previous insertions left (main.cpp:45-61 in row order)
+                        const uint32_t row0 = (uint32_t)(row - lane);
+                        do {
+                            const int b = __builtin_ctzll(m);
+                            m &= m - 1;
+                            const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc[i]), b));
+                            if (x < thr[i]) {
+                                shift_insert(T[i][0], ((u64)__float_as_uint(x) << 32) | (u64)(row0 + (uint32_t)b),
+                                             lane < k);
+                                thr[i] = kth_dist(T[i][0], k);
+                            }
+                        } while (m);
+                    } else {
+                        topk_merge<R>(T[i], pass ? make_key(acc[i], (uint32_t)row) : KEY_NONE);
+                        if constexpr (SH) {
+                            thr[i] = kth_dist(T[i][0], k);
+                        } else {
+                            const u64 kth = list_at(T[i], k - 1);
+                            thr[i] = kth == KEY_NONE ? FLT_MAX : __uint_as_float((uint32_t)(kth >> 32));
+                        }
+                    }
                 }
                 acc[i] = 0.0f;
             }
@@ -1872,13 +1922,13 @@ size_t knn_direct_tile_lds(int d, int C) {
     return 2 * 64 * (size_t)stride * 4 + (C <= KNN_VOTE_LDS_MAX_C ? (size_t)DT_NW * ((C + 3) & ~3) * 4 : 0);
 }
 
-template <int QW, int R, typename E>
-static const void* direct_tile_fn() { return reinterpret_cast<const void*>(&k_direct_tile<QW, R, E>); }
+template <int QW, int R, typename E, bool SH = false>
+static const void* direct_tile_fn() { return reinterpret_cast<const void*>(&k_direct_tile<QW, R, E, SH>); }
 
 template <typename E>
 static const void* direct_tile_fn_e(int k) {
     switch (list_regs(k)) {
-        case 1: return direct_tile_fn<8, 1, E>();
+        case 1: return k <= 16 ? direct_tile_fn<8, 1, E, true>() : direct_tile_fn<8, 1, E>();
         case 2: return direct_tile_fn<4, 2, E>();
         case 4: return direct_tile_fn<2, 4, E>();
         case 8: return direct_tile_fn<1, 8, E>();

@@ -24,7 +24,7 @@ def test_library_exports_every_header_symbol(knn):
     assert len(syms) >= 14
     for s in syms:
         assert hasattr(lib, s), s
-    assert lib.knn_version() == 2
+    assert lib.knn_version() == 3
 
 
 def test_library_built_from_this_tree(knn):
@@ -176,6 +176,21 @@ def test_c_shard_range_and_exchange_layout(knn):
         knn.exchange_layout(10, 0, 2, 0)
     with pytest.raises(knn.KnnError):
         knn.shard_range_c(10, 2, 2)
+
+
+def test_shard_policy_rule(knn):
+    """knn_shard_policy (north_star "Partitioning"): test-sharded while train and its bf16 filter
+    operands fit half of one GPU's HBM, train-sharded beyond; one GPU is always test-sharded."""
+    G = 288 << 30
+    assert knn.shard_policy(1_000_000, 100_000, 128, "f32", 8) == "test"      # A: 0.77 GB
+    assert knn.shard_policy(4_000_000, 1_000_000, 64, "f32", 8) == "test"     # B
+    assert knn.shard_policy(32_000_000, 1_000_000, 256, "bf16", 8) == "test"  # C fits (32 GB)
+    assert knn.shard_policy(400_000_000, 1_000_000, 256, "bf16", 8) == "train"  # 409 GB
+    assert knn.shard_policy(400_000_000, 1_000_000, 256, "bf16", 1) == "test"
+    assert knn.shard_policy(32_000_000, 1_000, 256, "bf16", 8, hbm_bytes=16 << 30) == "train"
+    assert knn.shard_policy(32_000_000, 1_000, 256, "bf16", 8, hbm_bytes=G) == "test"
+    with pytest.raises(knn.KnnError):
+        knn.shard_policy(10, 10, 0, "f32", 2)
 
 
 # --- multi-threaded ingestion (SURVEY.md 8f row 1) ------------------------------------

@@ -317,6 +317,24 @@ def test_cli_large_k5():
         assert pred_sha([int(x) for x in f.read().split()]) == golden_manifest()["large_k5"]["sha256"]
 
 
+@pytest.mark.parametrize("ds,k,workers,shard", [("large", 5, 3, "train"), ("medium", 100, 4, "train"),
+                                                 ("large", 32, 2, "auto"), ("small", 3, 3, "test")])
+def test_cli_shard_policies(ds, k, workers, shard):
+    """knn_cli --shard=...: the C++ KNN() split over `workers` device contexts (rehearsed on one
+    GPU: KNN_AMD_SHARE_GPU=1), test-sharded by the reference's rule or train-sharded (each
+    worker's shard top-k, merged on worker 0 by (distance, global index)): the golden
+    predictions of the reference's serial KNN either way (main.cpp:25-85)."""
+    out_file = f"/tmp/knn_cli_pred_{ds}_k{k}_{shard}.txt"
+    env = dict(os.environ, KNN_CLI_PRED_OUT=out_file, KNN_AMD_SHARE_GPU="1")
+    r = subprocess.run([os.path.join(PKG_DIR, "knn_cli"), f"{DATA}/{ds}-train.arff", f"{DATA}/{ds}-test.arff",
+                        str(k), str(workers), f"--shard={shard}"], capture_output=True, text=True, env=env,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "-NN classifier for" in r.stdout
+    with open(out_file) as f:
+        assert pred_sha([int(x) for x in f.read().split()]) == golden_manifest()[f"{ds}_k{k}"]["sha256"]
+
+
 def test_full_size_config_a_sampled(knn, oracle):
     """BASELINE config A at full size (1M x 100k x 128, k=10) on device; 48 sampled queries
     checked bit-exactly against the oracle on the full train set."""

@@ -90,6 +90,62 @@ def test_train_operands_cached_across_calls(knn, oracle, dtype, d, k):
         ref.close()
 
 
+def test_generate_into_slice_invalidates_cache(knn):
+    """Context.generate writes through the C ABI, behind torch's version counter: a write into a
+    slice of a cached train tensor, from this context or from another one, must drop the cached
+    operands (the next call recomputes them and matches an uncached context bit for bit)."""
+    import torch
+    train, labels, test = _rows(knn, 30_000, 1_000, 128, 91)
+    ctx = knn.Context(0, algo="gemm_bf16", cache_train=True)
+    ref = knn.Context(0, algo="gemm_bf16")
+    other = knn.Context(0)
+    try:
+        _call(ctx, train, labels, test, 10)
+        assert _call(ctx, train, labels, test, 10)[3]["train_operands_cached"]
+        for writer, seed in ((ctx, 5), (other, 6)):
+            part = train[7_000:9_000]            # a view: another tensor object, same storage
+            writer.generate(part, None, 7_000, 128, 0, seed, 0, 10)
+            torch.cuda.synchronize()
+            got = _call(ctx, train, labels, test, 10)
+            assert not got[3]["train_operands_cached"], writer
+            assert _same(got, _call(ref, train, labels, test, 10))
+            assert _call(ctx, train, labels, test, 10)[3]["train_operands_cached"]
+        # a write elsewhere (another tensor) leaves the cache alone
+        spare = torch.empty_like(train[:100])
+        other.generate(spare, None, 0, 128, 0, 7, 0, 10)
+        torch.cuda.synchronize()
+        assert _call(ctx, train, labels, test, 10)[3]["train_operands_cached"]
+    finally:
+        ctx.close()
+        ref.close()
+        other.close()
+
+
+def test_cache_train_without_device_flag(knn):
+    """ABI 3: KNN_OPT_CACHE_TRAIN alone never reuses operands derived from a caller's device
+    buffer (only knn_predict's own upload); KNN_OPT_CACHE_TRAIN_DEVICE opts in."""
+    import ctypes
+    import torch
+    train, labels, test = _rows(knn, 30_000, 800, 128, 93)
+    lib = knn.load_library()
+    h = ctypes.c_void_p()
+    opts = knn.knn_opts(0, knn.ALGOS["gemm_bf16"], 0, 0, knn.KNN_OPT_CACHE_TRAIN)
+    assert lib.knn_create(ctypes.byref(h), ctypes.byref(opts)) == knn.KNN_OK
+    try:
+        tr = knn._device_dataset(train, labels)
+        te = knn._device_dataset(test)
+        pred = torch.empty(800, dtype=torch.int32, device=DEV)
+        st = torch.cuda.current_stream().cuda_stream
+        v = (ctypes.c_int64 * 9)()
+        for _ in range(2):
+            assert lib.knn_predict_device(h, ctypes.byref(tr), ctypes.byref(te), 10, 10, pred.data_ptr(),
+                                          None, None, ctypes.c_void_p(st)) == knn.KNN_OK
+            lib.knn_last_stats(h, v, 9)
+            assert v[5] == 1 and v[8] == 0  # fused filter ran, train operands rebuilt
+    finally:
+        lib.knn_destroy(h)
+
+
 def test_train_operands_cached_host_path(knn, oracle):
     """knn_predict with KNN_OPT_CACHE_TRAIN: a hit on the uploaded copy is also a hit on its
     filter operands; a new upload (generation) recomputes them."""
@@ -224,6 +280,7 @@ def test_comm_local_failure_vote_single_rank(knn, oracle):
         st = ctx.lib.knn_predict_train_sharded(ctx.h, comm.h, ctypes.byref(tr), 0, ctypes.byref(te), 5, 10,
                                                None, None, None, None)
         assert st == knn.KNN_EINVAL
+        assert not comm.broken()  # a voted local failure leaves the communicator healthy
         pred = torch.empty(300, dtype=torch.int32, device=DEV)
         comm.predict_train_sharded(train, labels, 0, test, 5, 10, pred)
         torch.cuda.synchronize()
