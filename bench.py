@@ -74,20 +74,24 @@ def _ref_exe(name):
     return os.path.join(REPO, "oracle", "_ref", name)
 
 
-def cpu_baseline(d, k, C, seed, kind=0):
+def cpu_baseline(d, k, C, seed, kind=0, nt_cfg=1_000_000):
     """Reference pthreads KNN (multi-thread.cpp:37) on a bounded sample of the workload,
     beside it the same sample through the reference's -O2 build (ref_bench_O2) and the
     reference's MPI path (mpi.cpp:141-186, ref_bench_mpi under mpiexec, as many ranks as
-    threads)."""
+    threads).  Sample: the full train set up to 1M rows x 8 T queries (T
+    threads, a multiple of T so the remainder rule does not skew); the MPI leg, whose every
+    rank builds its own libarff copy of train (~10 GB per 1M x 128 rows), uses 100k train
+    rows x 64 T queries."""
     threads = int(os.environ.get("KNN_BENCH_CPU_THREADS", min(16, os.cpu_count() or 1)))
-    # ~1e8 pairs at d=128 (10-30 s of CPU work at -O0); fewer train rows at larger d
-    nt_s, nq_s = 100_000 * 128 // max(d, 128), 64 * threads
+    nt_s, nq_s = min(nt_cfg, 1_000_000), 8 * threads
     exe = _ref_exe("ref_bench")
     sample = f"{nq_s} queries x {nt_s} train rows (d={d}, k={k}) of the same generator"
     argv = [str(kind), str(seed), str(nt_s), str(nq_s), str(d), str(k), str(C)]
+    nt_m, nq_m = 100_000 * 128 // max(d, 128), 64 * threads
+    argv_m = [str(kind), str(seed), str(nt_m), str(nq_m), str(d), str(k), str(C)]
 
     def run(cmd):
-        out = subprocess.run(cmd, capture_output=True, text=True, check=True, timeout=600)
+        out = subprocess.run(cmd, capture_output=True, text=True, check=True, timeout=900)
         return json.loads(out.stdout.strip().splitlines()[-1])
 
     if os.path.exists(exe):
@@ -101,11 +105,11 @@ def cpu_baseline(d, k, C, seed, kind=0):
                          "queries_per_s": r2["queries_per_s"],
                          "note": "the same sample through multi-thread.cpp built -O2"}
         if os.path.exists(_ref_exe("ref_bench_mpi")) and os.path.exists(MPIEXEC):
-            r3 = run([MPIEXEC, "-n", str(threads), _ref_exe("ref_bench_mpi")] + argv)
+            r3 = run([MPIEXEC, "-n", str(threads), _ref_exe("ref_bench_mpi")] + argv_m)
             rec["mpi"] = {"value": r3["pairs_per_s"], "unit": "pairs/s", "cores": threads,
                           "queries_per_s": r3["queries_per_s"],
-                          "note": f"the same sample through mpi.cpp's KNN + Scatter/Gatherv, -O0, MPICH, "
-                                  f"mpiexec -n {threads}"}
+                          "note": f"{nq_m} queries x {nt_m} train rows through mpi.cpp's KNN + Scatter/Gatherv, "
+                                  f"-O0, MPICH, mpiexec -n {threads} (every rank holds its own train copy)"}
         else:
             rec["mpi"] = "absent"
         return rec
@@ -594,7 +598,7 @@ def main():
                 roof["x_fp32_mfma_peak"] = round(ach / MFMA_PEAK_TFLOPS["f32"], 3)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(d, k, C, seed, kind)
+            cpu = cpu_baseline(d, k, C, seed, kind, nt)
         par = (f"test-sharded dp{world}, train replicated" if sharding == "test" else
                f"train-sharded x{world} (shard_range of train rows), all-to-all of per-shard top-k "
                f"({'RCCL via knn_predict_train_sharded' if comm is not None else 'torch.distributed'}), merge")

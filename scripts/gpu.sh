@@ -34,7 +34,7 @@ for spec in "${SPECS[@]}"; do
   EV=(); AR=()
   for w in "${W[@]:2}"; do if [[ $w == --* ]]; then AR+=("$w"); else EV+=("$w"); fi; done
   env "${EV[@]}" timeout -k 10 400 python -u bench.py --config $cfg --steps ${STEPS:-3} --warmup ${WARMUP:-1} \
-      --no-cpu-baseline --no-host-path "${AR[@]}" > gpurun_out/${TAG}_$tag.log 2>&1 \
+      --no-cpu-baseline --no-host-path --no-bit-match --no-uncached "${AR[@]}" > gpurun_out/${TAG}_$tag.log 2>&1 \
       || { echo "bench $tag failed"; tail -5 gpurun_out/${TAG}_$tag.log; exit 1; }
   summ gpurun_out/${TAG}_$tag.log
 done

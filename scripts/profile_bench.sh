@@ -14,7 +14,7 @@ STEPS=${STEPS:-2}
 cd /tmp && export TMPDIR=/tmp
 OUT=$R/gpurun_out
 PT=${PROF_TAG:-prof}   # output dirs $OUT/${PT}_{trace,fetch,write,sq}
-BENCH="$R/bench.py --steps $STEPS --warmup 1 --no-cpu-baseline --no-host-path ${BENCH_ARGS:-}"
+BENCH="$R/bench.py --steps $STEPS --warmup 1 --no-cpu-baseline --no-host-path --no-bit-match --no-uncached ${BENCH_ARGS:-}"
 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${PT}_trace -o run \
     -- python3 $BENCH > $OUT/${PT}_trace.log 2>&1 || { echo "trace pass failed"; exit 1; }

@@ -17,8 +17,11 @@ lib.knn_debug_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_in
 buf = (ctypes.c_ulonglong * 8)()
 dev = torch.device("cuda", 0)
 # (C1s: config C1's shard shape -- 4M bf16 rows x 256-d, k = 100 -- on 65,536 queries)
-for name, nt, nq, d, k, seed, bf in [("A", 1_000_000, 100_000, 128, 10, 1, 0), ("B", 4_000_000, 1_000_000, 64, 32, 2, 0),
-                                      ("C1s", 4_000_000, 65_536, 256, 100, 3, 1)]:
+# (As: A's 8-GPU share, 12,500 queries; STAMPS_CONFIGS=A,As selects)
+ALL = [("A", 1_000_000, 100_000, 128, 10, 1, 0), ("As", 1_000_000, 12_500, 128, 10, 1, 0),
+       ("B", 4_000_000, 1_000_000, 64, 32, 2, 0), ("C1s", 4_000_000, 65_536, 256, 100, 3, 1)]
+pick = os.environ.get("STAMPS_CONFIGS")
+for name, nt, nq, d, k, seed, bf in [c for c in ALL if not pick or c[0] in pick.split(",")]:
     ctx = knn.Context(0, algo="auto", profile=True)
     dt = torch.bfloat16 if bf else torch.float32
     train = torch.empty((nt, d), dtype=dt, device=dev)
@@ -38,6 +41,7 @@ for name, nt, nq, d, k, seed, bf in [("A", 1_000_000, 100_000, 128, 10, 1, 0), (
     print(f"{name}: filter {st.get('gemm_filter', 0):.2f} ms; per wave-piece sums over {waves} wave-pieces: "
           f"barrier {bar / piece:.3f}, step {step / piece:.3f}, slow {slow / piece:.3f} of the piece cycles; "
           f"tiles with a slow path {slow_tiles / tiles:.3f}; slow cycles per such tile {slow / max(slow_tiles, 1):.0f}; "
-          f"step cycles per tile {step / tiles:.0f}; barrier cycles per tile {bar / tiles:.0f}", flush=True)
+          f"step cycles per tile {step / tiles:.0f}; barrier cycles per tile {bar / tiles:.0f}; "
+          f"other (exchanges, piece set-up, drain) {(piece - bar - step - slow) / piece:.3f}", flush=True)
     ctx.close()
     del train, labels, test, pred
