@@ -258,11 +258,21 @@ knn_status finish_call(knn_ctx* c, hipStream_t st) {
 // resident blocks (more segments only when they raise the filled fraction by > 2 %, each
 // one costs a merge pass), at least 4 tiles per segment, records within 2 GB
 int choose_direct_segments(const knn_ctx* c, int64_t nt, int64_t nq, int d, int k, int C, int elem) {
-    const int qb = knn_direct_tile_qb(k);
+    int qb = 1, occ = 1;
+    if (knn_direct_units(k, elem, d, C, &qb, &occ) != hipSuccess || occ < 1) occ = 1;
     const int64_t nqb = (nq + qb - 1) / qb;
-    int occ = 1;
-    if (knn_direct_tile_occupancy(k, elem, d, C, &occ) != hipSuccess || occ < 1) occ = 1;
     const int64_t slots = (int64_t)occ * c->num_cus;
+    if (qb < knn_direct_tile_qb(k)) {
+        // k_direct_rows (a wave per unit): enough units for half the resident waves -- its
+        // waves need no co-residents to hide a barrier, and every segment adds a sorted first
+        // tile and a merge source (config L, 430 query groups: 4 segments 0.101 ms, 8 0.097,
+        // 16 (a full round) 0.104, 32 0.131; r05c)
+        const int64_t want = (slots / 2 + nqb - 1) / nqb;
+        int64_t s = std::max<int64_t>(1, std::min<int64_t>(want, 32));
+        while (s > 1 && nt / s < 256) s--;
+        while (s > 1 && (double)s * (double)nq * 12.0 * k > 2e9) s--;
+        return (int)s;
+    }
     int best = 1;
     double best_eff = 0.0;
     for (int s = 1; s <= 32; s++) {

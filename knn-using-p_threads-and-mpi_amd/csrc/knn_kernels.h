@@ -119,7 +119,11 @@ int knn_direct_tile_qb(int k);
 // launch geometry: LDS bytes per block and blocks per CU at that LDS
 size_t knn_direct_tile_lds(int d, int C);
 hipError_t knn_direct_tile_occupancy(int k, int elem, int d, int C, int* blocks_per_cu);
-// fills dc / stride / vote_lds / n_qblocks from d, C, nq and launches nseg * n_qblocks blocks
+// work units of the direct form for (k, d): queries per unit and units resident per CU --
+// k_direct_tile: a block of 8 waves; k_direct_rows (d <= 16, k <= 16): one wave
+hipError_t knn_direct_units(int k, int elem, int d, int C, int* queries_per_unit, int* units_per_cu);
+// fills dc / stride / vote_lds / n_qblocks from d, C, nq and launches nseg units per query
+// unit (k_direct_tile: blocks; k_direct_rows for d <= 16, k <= 16: waves, four per block)
 hipError_t knn_launch_direct_tile(DirectTileArgs a, hipStream_t st);
 
 struct GenerateArgs {

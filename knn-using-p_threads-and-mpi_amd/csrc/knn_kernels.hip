@@ -513,6 +513,163 @@ __global__ __launch_bounds__(64 * DT_NW, 4) void k_direct_tile(DirectTileArgs a)
         }
     }
 }
+
+// ---------------------------------------------------------------------------------
+// k_direct_rows<NG, QW, E>: the direct form for d <= 16 and k <= 16 (NG = ceil(d / 4) groups of
+// four features; config L: d = 11, k = 5).  Such rows are 16-64 bytes, so the tile kernel's LDS
+// staging and per-tile block barrier cost more than the arithmetic they feed.  Here every wave
+// is independent -- no LDS, no barrier: lane = train row, each lane loads its own row (NG
+// float4; the rows of a tile are contiguous across the lanes, one coalesced read) two tiles
+// ahead of its use, and the wave's QW queries are loop-invariant registers.  The arithmetic
+// runs on query PAIRS in packed fp32 (v_pk_add_f32 / v_pk_mul_f32: two lanes of IEEE fp32 per
+// instruction, each rounded exactly like the scalar op), so the sub, mul, add of
+// main.cpp:14-23 cost 1.5 instructions per dimension per query instead of 3 -- the same bits.
+// Selection: the lane-shift insert of k_direct_tile's SH path.  Work unit = one wave = (QW
+// queries, one train segment): wave u of the grid takes query group u % n_qb and segment
+// u / n_qb, so the waves one CU runs at once share a segment's rows in L2.
+// ---------------------------------------------------------------------------------
+typedef float f2v __attribute__((ext_vector_type(2)));
+template <int NG, int QW, typename E>
+__global__ __launch_bounds__(256) void k_direct_rows(DirectTileArgs a) {
+    static_assert(QW % 2 == 0, "queries go in pairs");
+    constexpr int QP = QW / 2;
+    const int lane = lane_id();
+    const int64_t u = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int qg = (int)(u % a.n_qblocks);
+    const int seg = (int)(u / a.n_qblocks);
+    if (seg >= a.nseg) return;  // (wave-uniform: the grid's last block may be partial)
+    const int64_t row_begin = (int64_t)seg * a.seg_len;
+    const int64_t row_end = min(a.nt, row_begin + a.seg_len);
+    const E* __restrict__ train = reinterpret_cast<const E*>(a.train);
+    const E* __restrict__ test = reinterpret_cast<const E*>(a.test);
+    const int d = a.d, k = a.k;
+    const int rem = d - 4 * (NG - 1);  // features in the last group, 1..4
+
+    int64_t qi[QW];
+    f2v qv[QP][4 * NG];  // query pair p, feature c: (q_2p[c], q_2p+1[c]); zero past d
+#pragma unroll
+    for (int i = 0; i < QW; i++) qi[i] = (int64_t)qg * QW + i;
+#pragma unroll
+    for (int p = 0; p < QP; p++) {
+        const E* r0 = test + min(qi[2 * p], a.nq - 1) * (int64_t)a.ld_q;
+        const E* r1 = test + min(qi[2 * p + 1], a.nq - 1) * (int64_t)a.ld_q;
+#pragma unroll
+        for (int g = 0; g < NG; g++) {
+            const float4 x = load4(r0 + 4 * g), y = load4(r1 + 4 * g);
+            qv[p][4 * g + 0] = f2v{x.x, y.x};
+            qv[p][4 * g + 1] = f2v{x.y, y.y};
+            qv[p][4 * g + 2] = f2v{x.z, y.z};
+            qv[p][4 * g + 3] = f2v{x.w, y.w};
+        }
+    }
+    u64 T[QW][1];
+    float thr[QW];
+#pragma unroll
+    for (int i = 0; i < QW; i++) {
+        T[i][0] = KEY_NONE;
+        thr[i] = FLT_MAX;  // main.cpp:33: the FLT_MAX sentinel
+    }
+    const int64_t nrows = row_end > row_begin ? row_end - row_begin : 0;
+    const int ntiles = (int)((nrows + 63) >> 6);
+    auto load_row = [&](int t, float4 (&x)[NG]) __attribute__((always_inline)) {
+        const int64_t r = min(row_begin + 64 * (int64_t)t + lane, row_end - 1);
+#pragma unroll
+        for (int g = 0; g < NG; g++) x[g] = load4(train + r * a.ld_t + 4 * g);
+    };
+    float4 buf[3][NG];  // rows of tiles t, t+1, t+2 (loads two tiles ahead)
+    if (ntiles > 0) load_row(0, buf[0]);
+    if (ntiles > 1) load_row(1, buf[1]);
+    auto dist = [&](const float4 (&x)[NG], f2v (&acc)[QP]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int p = 0; p < QP; p++) acc[p] = f2v{0.0f, 0.0f};
+#pragma unroll
+        for (int g = 0; g < NG; g++) {
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                if (g == NG - 1 && c >= rem) break;  // (wave-uniform)
+                const float tv = f4get(x[g], c);
+#pragma unroll
+                for (int p = 0; p < QP; p++) {
+                    const f2v df = qv[p][4 * g + c] - f2v{tv, tv};
+                    acc[p] = acc[p] + df * df;
+                }
+            }
+        }
+    };
+    // tile 0 of the segment: every row passes the FLT_MAX sentinel, so each list starts as the
+    // sorted tile (one bitonic sort, KEY_NONE for rows past the segment) -- after it the lists
+    // are full and every later tile goes through the lane shift, one passing row at a time
+    // (a tile with many passing rows, rare past tile 0, just takes more rounds)
+    auto first = [&](const float4 (&x)[NG]) __attribute__((always_inline)) {
+        f2v acc[QP];
+        dist(x, acc);
+        const int64_t row = row_begin + lane;
+        const bool valid = row < row_end;
+#pragma unroll
+        for (int i = 0; i < QW; i++) {
+            const float di = (i & 1) ? acc[i >> 1].y : acc[i >> 1].x;
+            T[i][0] = sort64(valid ? make_key(di, (uint32_t)row) : KEY_NONE, /*descending=*/false);
+            thr[i] = kth_dist(T[i][0], k);
+        }
+    };
+    auto tile = [&](int t, const float4 (&x)[NG]) __attribute__((always_inline)) {
+        f2v acc[QP];
+        dist(x, acc);
+        const int64_t row = row_begin + 64 * (int64_t)t + lane;
+        const bool valid = row < row_end;
+        const uint32_t row0 = (uint32_t)(row - lane);
+#pragma unroll
+        for (int i = 0; i < QW; i++) {
+            const float di = (i & 1) ? acc[i >> 1].y : acc[i >> 1].x;
+            u64 m = __ballot(valid && di < thr[i]);
+            while (m) {
+                const int b = __builtin_ctzll(m);
+                m &= m - 1;
+                const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(di), b));
+                if (x < thr[i]) {  // (re-tested against the threshold the earlier rows left)
+                    shift_insert(T[i][0], ((u64)__float_as_uint(x) << 32) | (u64)(row0 + (uint32_t)b), lane < k);
+                    thr[i] = kth_dist(T[i][0], k);
+                }
+            }
+        }
+    };
+    if (ntiles > 2) load_row(2, buf[2]);
+    if (ntiles > 0) first(buf[0]);
+    // tiles 1, 2, ...: loads two tiles ahead into three static buffer places (no register copies)
+    int t = 1;
+    for (; t + 3 <= ntiles; t += 3) {
+        if (t + 2 < ntiles) load_row(t + 2, buf[0]);
+        tile(t, buf[1]);
+        if (t + 3 < ntiles) load_row(t + 3, buf[1]);
+        tile(t + 1, buf[2]);
+        if (t + 4 < ntiles) load_row(t + 4, buf[2]);
+        tile(t + 2, buf[0]);
+    }
+    if (t < ntiles) {
+        if (t + 2 < ntiles) load_row(t + 2, buf[0]);
+        tile(t, buf[1]);
+        if (t + 1 < ntiles) tile(t + 1, buf[2]);
+    }
+    if (a.nseg == 1) {
+#pragma unroll
+        for (int i = 0; i < QW; i++)
+            if (qi[i] < a.nq) finish_query<1>(T[i], k, a.C, a.labels, nullptr, qi[i], a.out, a.status);
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < QW; i++) {
+        if (qi[i] >= a.nq) continue;
+        int32_t* rec = a.rec + ((int64_t)seg * a.nq + qi[i]) * 3 * (int64_t)k;
+        if (lane < k) {
+            const u64 key = T[i][0];
+            const bool none = key == KEY_NONE;
+            const int32_t idx = (int32_t)(uint32_t)(key & 0xffffffffull);
+            rec[lane] = none ? (int32_t)__float_as_uint(FLT_MAX) : (int32_t)(uint32_t)(key >> 32);
+            rec[k + lane] = none ? -1 : idx;
+            rec[2 * k + lane] = none ? -1 : a.labels[idx];
+        }
+    }
+}
 #pragma clang fp contract(on)
 
 
@@ -1939,14 +2096,57 @@ static const void* direct_tile_ptr(int k, int elem) {
     return elem == ELEM_BF16 ? direct_tile_fn_e<bf16_t>(k) : direct_tile_fn_e<float>(k);
 }
 
+// k_direct_rows (d <= 16, k <= 16): DR_QW queries per wave (their features stay in scalar
+// registers), a wave per work unit
+static constexpr int DR_QW = 4;
+static bool direct_rows(int k, int d) { return d <= 16 && k <= 16; }
+template <typename E>
+static const void* direct_rows_fn(int d) {
+    switch ((d + 3) / 4) {
+        case 1: return reinterpret_cast<const void*>(&k_direct_rows<1, DR_QW, E>);
+        case 2: return reinterpret_cast<const void*>(&k_direct_rows<2, DR_QW, E>);
+        case 3: return reinterpret_cast<const void*>(&k_direct_rows<3, DR_QW, E>);
+        default: return reinterpret_cast<const void*>(&k_direct_rows<4, DR_QW, E>);
+    }
+}
+static const void* direct_rows_ptr(int d, int elem) {
+    return elem == ELEM_BF16 ? direct_rows_fn<bf16_t>(d) : direct_rows_fn<float>(d);
+}
+
 hipError_t knn_direct_tile_occupancy(int k, int elem, int d, int C, int* blocks_per_cu) {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, direct_tile_ptr(k, elem), 64 * DT_NW,
                                                         knn_direct_tile_lds(d, C));
 }
 
+hipError_t knn_direct_units(int k, int elem, int d, int C, int* queries_per_unit, int* units_per_cu) {
+    int occ = 1;
+    hipError_t e;
+    if (direct_rows(k, d)) {
+        *queries_per_unit = DR_QW;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, direct_rows_ptr(d, elem), 256, 0);
+        *units_per_cu = 4 * std::max(occ, 1);
+    } else {
+        *queries_per_unit = knn_direct_tile_qb(k);
+        e = knn_direct_tile_occupancy(k, elem, d, C, &occ);
+        *units_per_cu = std::max(occ, 1);
+    }
+    return e;
+}
+
 hipError_t knn_launch_direct_tile(DirectTileArgs a, hipStream_t st) {
     if (a.nq <= 0) return hipSuccess;
     if (a.nseg < 1 || (a.nseg > 1 && !a.rec) || a.d < 1 || a.k < 1 || a.k > 1024) return hipErrorInvalidValue;
+    if (direct_rows(a.k, a.d)) {
+        // the wave-per-unit shape: n_qblocks query groups of DR_QW, 4 units per block
+        a.n_qblocks = (int)((a.nq + DR_QW - 1) / DR_QW);
+        const int64_t units = (int64_t)a.n_qblocks * a.nseg;
+        void* args[] = {&a};
+        hipError_t e = hipLaunchKernel(direct_rows_ptr(a.d, a.elem), dim3((unsigned)((units + 3) / 4)), dim3(256), args,
+                                       0, st);
+        if (e != hipSuccess) return e;
+        KNN_LAUNCH_CHECK();
+        return hipSuccess;
+    }
     direct_tile_geom(a.d, &a.dc, &a.stride);
     a.vote_lds = a.C <= KNN_VOTE_LDS_MAX_C;
     const int qb = knn_direct_tile_qb(a.k);

@@ -24,7 +24,7 @@ test[:, :d] = torch.from_numpy(qf).to(dev)
 labels = torch.from_numpy(tl).to(dev)
 C = int(tl.max()) + 1
 ref = None
-for splits in (0, 1, 4, 8, 18, 32):
+for splits in (0, 4, 8, 12, 16, 24, 32):
     ctx = knn.Context(0, algo="direct", train_splits=splits, profile=3)
     pred = torch.empty(nq, dtype=torch.int32, device=dev)
     for _ in range(3):
