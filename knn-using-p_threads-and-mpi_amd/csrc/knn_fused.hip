@@ -42,6 +42,9 @@ static constexpr int FUSED_RQ = 4;            // queued passing values per lane 
 #ifndef KNN_FUSED_LIST_FIRST
 #define KNN_FUSED_LIST_FIRST 31               // first list exchange after this tile (then doubling)
 #endif
+#ifndef KNN_FUSED_DMA_FRONT
+#define KNN_FUSED_DMA_FRONT 0                 // (study) a group's tile DMAs all issued right after its barrier
+#endif
 #ifndef KNN_FUSED_LIST_EVERY
 #define KNN_FUSED_LIST_EVERY (1 << 30)        // list exchanges: tiles 32, 64, 128, ... (+ every this many)
 #endif
@@ -942,7 +945,30 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         // this tile's terms, for its fast test in the next iteration (the tile is resident:
         // landed before this step's barrier, not overwritten before the next one)
         const TQ tm_cur = tile_q(it % NBUF);
-        const bool dma_on = !KNN_STUDY_NO_DMA && it + AHEAD < ntiles;
+        // Tile DMAs.  Spread (the round-4 order): step it issues tile it + AHEAD's pieces between
+        // its MFMAs -- so the next group's last tile goes out in the last step before the
+        // barrier that waits for it (vmcnt(0)), and its whole memory latency is exposed at every
+        // group barrier.  Front (KNN_FUSED_DMA_FRONT, groups of GRP >= 2 tiles): right after a
+        // group's barrier, when the previous group's buffers are free, every tile of the NEXT
+        // group is issued at once, so each has a whole group's compute to land.  Measured slower
+        // everywhere (r05d, same box: A 20.56 -> 21.03 ms, B 479.6 -> 493.2, C1 1729 -> 1796, A's
+        // 8-GPU share 3.27 -> 3.39): the barrier wait is the waves' slow-path skew, not the last
+        // DMA's latency, and the burst lands on the group's first fragment reads.  A study build.
+        constexpr bool FRONT = KNN_FUSED_DMA_FRONT && PAIR;
+        if constexpr (FRONT) {
+            if (POS == 0 && !KNN_STUDY_NO_DMA) {
+#pragma unroll
+                for (int p = 0; p < GRP; p++) {
+                    const int tn = it + GRP + p;
+                    if (tn < ntiles) {
+                        const DmaTile dp = dma_desc(tn % NBUF, tn);
+#pragma unroll
+                        for (int i = 0; i < DMA_PER_WAVE; i++) dma_piece(i, dp);
+                    }
+                }
+            }
+        }
+        const bool dma_on = !FRONT && !KNN_STUDY_NO_DMA && it + AHEAD < ntiles;
         const DmaTile dd = dma_desc((it + AHEAD) % NBUF, it + AHEAD);
         float tf[QG];
 #pragma unroll
