@@ -4,11 +4,13 @@
 
 One process per GPU (torchrun for N > 1).  Workload A (default, BASELINE configs[2]):
 1,000,000 train x 100,000 query rows x 128-d fp32, k = 10, 10 classes, synthetic rows from
-the counter-based generator generated directly in HBM.  On N GPUs the fixed
-test set is split by the reference's rule (rank r owns shard_range(100k, N, r),
-multi-thread.cpp:154-158 / mpi.cpp:141-170) with train replicated: strong scaling with no
-data-path collective (the reference's MPI_Gatherv of predictions, mpi.cpp:186, is not part
-of the timed region).  --weak gives every rank 100,000 queries of its own instead.  A
+the counter-based generator generated directly in HBM.  The path partitions by
+query (north_star: test-sharded, train replicated, no data-path collective; the reference's
+MPI_Gatherv of predictions, mpi.cpp:186, is not part of the timed region), so on N GPUs every
+rank owns 100,000 queries of its own (global rows [r*100k, (r+1)*100k)) against the same train
+set: weak scaling, "scaling": "weak" (the contract for a partitioned path).  --strong splits
+the fixed 100k-query set by the reference's rule instead (rank r owns shard_range(100k, N, r),
+multi-thread.cpp:154-158 / mpi.cpp:141-170): the reference's own fixed-problem speed-up.  A
 "step" is one KNN(train, test, k) pass over the resident inputs: norms -> MFMA filter ->
 exact rescore/vote -> fallback.  B (configs[3]) is the same split of 1M queries over a 4M-row
 train set.
@@ -45,8 +47,8 @@ sys.path.insert(0, REPO)
 
 CONFIGS = {
     # name: (n_train, n_query (per GPU when weak), d, k, classes, seed, scaling, dtype, sharding)
-    "A": (1_000_000, 100_000, 128, 10, 10, 1, "strong", "f32", "test"),
-    "B": (4_000_000, 1_000_000, 64, 32, 10, 2, "strong", "f32", "test"),
+    "A": (1_000_000, 100_000, 128, 10, 10, 1, "weak", "f32", "test"),
+    "B": (4_000_000, 1_000_000, 64, 32, 10, 2, "weak", "f32", "test"),
     "C": (32_000_000, 1_000_000, 256, 100, 10, 3, "strong", "bf16", "train"),
     "C1": (4_000_000, 1_000_000, 256, 100, 10, 3, "strong", "bf16", "train"),
     "L": (30_803, 1_718, 11, 5, 10, 0, "strong", "f32", "arff"),
@@ -242,17 +244,22 @@ def bench_arff(args, knn, torch, local):
     cm = knn.computeConfusionMatrix(got, ql, C)
     pairs = float(nt) * nq * args.steps
     stages = {n: v / args.steps for n, v in stage_sum.items()}
-    # the dominant kernel: AUTO picks the direct form (k_direct_tile) or the exact scan here
+    # the dominant kernel: AUTO picks the direct form here -- k_direct_rows for d <= 16, k <= 16
+    # (config L), else k_direct_tile -- its segments merged by k_merge_vote (stage "merge_vote")
     kname = "direct_tile" if "direct_tile" in stages else "exact_scan"
     scan = stages.get(kname)
     roof = None
     if scan:
         ops = 3.0 * d * nt * nq  # sub, mul, add per dimension per pair (unfused: the reference's bits)
+        kernel = ("k_direct_rows" if d <= 16 and k <= 16 else "k_direct_tile") if kname == "direct_tile" \
+            else "k_exact_scan"
         roof = {"bound": "valu", "achieved": round(ops / (scan * 1e-3) / 1e12, 3), "peak": 78.6,
                 "unit": "Tops/s", "frac": round(ops / (scan * 1e-3) / 1e12 / 78.6, 4), "traffic": None,
-                "kernel": "k_" + kname, "avg_launch_ms": round(scan, 4),
-                "peak_basis": "fp32 VALU, non-FMA ops: 256 CUs x 4 SIMDs x 32 lanes/clk at 2.4 GHz "
-                              "(MI355X_MICROARCH.md: 157.3 TFLOP/s counting an FMA as 2)",
+                "kernel": kernel, "avg_launch_ms": round(scan, 4),
+                "peak_basis": "fp32 VALU: 256 CUs x 4 SIMDs x 32 lanes/clk at 2.4 GHz, packed fp32 "
+                              "(v_pk_add/mul_f32: two ops per lane) -- MI355X_MICROARCH.md: 157.3 TFLOP/s "
+                              "counting an FMA as 2",
+                "merge_ms": round(stages.get("merge_vote", 0.0), 4),
                 "note": "launch/latency bound: 52.9 M pairs is ~22 us of VALU at peak"}
     out = {
         "metric": METRIC, "value": pairs / elapsed, "unit": "pairs/s", "n_gpus": 1,
@@ -341,8 +348,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default: per config)")
     ap.add_argument("--config", default="A", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--weak", action="store_true",
-                    help="test-sharded configs: every rank owns n_query rows of its own (weak scaling)")
+    ap.add_argument("--strong", action="store_true",
+                    help="test-sharded configs: split the fixed n_query set by the reference's rule "
+                         "(strong scaling) instead of giving every rank n_query rows of its own")
+    ap.add_argument("--weak", action="store_true", help="(the default for test-sharded configs)")
     ap.add_argument("--exchange", default="rccl", choices=["rccl", "torch"],
                     help="train-sharded configs: C-ABI RCCL communicator or torch.distributed all-to-all")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-buffer calls")
@@ -403,8 +412,10 @@ def main():
                                     torch.cuda.get_device_properties(local).total_memory)
     elif args.shard:
         sharding = args.shard
-    if args.weak and sharding == "test":
-        scaling = "weak"
+    if sharding == "test":
+        scaling = "strong" if args.strong else "weak"
+    else:
+        scaling = "strong"
     kind = 1 if dtype == "bf16" else 0                  # bf16-exact generator values for bf16
     tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
     dev = torch.device("cuda", local)

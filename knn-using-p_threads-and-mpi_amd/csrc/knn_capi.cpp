@@ -306,6 +306,9 @@ knn_status run_direct_tile(knn_ctx* c, const knn_dataset* tr, const knn_dataset*
     HIP_OR_FAIL(c, c->seg_rec.ensure(sizeof(int32_t) * 3 * (size_t)k * (size_t)te->n * nseg));
     a.rec = c->seg_rec.as<int32_t>();
     HIP_OR_FAIL(c, knn_launch_direct_tile(a, st));
+    // (the merge is its own stage: "direct_tile" times the distance kernel alone)
+    stage_end(c, st);
+    stage_begin(c, st, "merge_vote");
     MergeArgs m{};
     m.rec = a.rec; m.nsrc = nseg; m.nq = te->n; m.k = k; m.C = C;
     m.out = out; m.status = a.status; m.labels = tr->labels;
