@@ -88,7 +88,9 @@ struct knn_ctx {
     bool no_lshare = false, no_cursor = false, rescore_all = false;
     // host-API staging (device copies of host inputs / outputs)
     DBuf h_train, h_labels, h_test, h_pred, h_dist, h_idx;
-    int32_t* ctrl_host = nullptr;  // pinned: [0] status, [1] fallback count
+    int32_t* ctrl_host = nullptr;  // pinned, mapped, fine-grained: [0] status, [1] fallback count
+    int32_t* ctrl_host_dev = nullptr;  // its device address (k_finish writes it)
+    bool ctrl_clean = false;  // the status words are zero (the last call ended in k_finish)
     // host-buffer calls (knn_predict): cached train upload, two query slots streamed on a copy stream
     int cache_train = 0;
     uint64_t generation = 0;
@@ -246,12 +248,21 @@ knn_status check_status(knn_ctx* c, const int32_t* ctrl) {
     return KNN_OK;
 }
 
-// the one host synchronisation of a call: status word to the host, stream drained
+// the one host synchronisation of a call: k_finish writes the status words to the host's
+// mapped copy and zeroes them for the next call, then the stream drains
 knn_status finish_call(knn_ctx* c, hipStream_t st) {
-    HIP_OR_FAIL(c, hipMemcpyAsync(c->ctrl_host, c->ctrl.p, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(c, knn_launch_finish(c->ctrl.as<int32_t>(), c->ctrl_host_dev, 4, st));
     HIP_OR_FAIL(c, hipStreamSynchronize(st));
+    c->ctrl_clean = true;
     collect_stages(c);
     return check_status(c, c->ctrl_host);
+}
+// a call's first enqueue: the status words start at zero (k_finish left them so, unless the last
+// call failed before it ran)
+hipError_t reset_ctrl(knn_ctx* c, hipStream_t st) {
+    const bool clean = c->ctrl_clean;
+    c->ctrl_clean = false;
+    return clean ? hipSuccess : hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st);
 }
 
 // k_direct_tile segments: enough (query block, segment) units to fill whole waves of
@@ -732,7 +743,9 @@ knn_status knn_create(knn_ctx** out, const knn_opts* opts) {
     c->num_cus = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void**)&c->ctrl_host, 4 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&c->ctrl_host, 4 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer((void**)&c->ctrl_host_dev, c->ctrl_host, 0) != hipSuccess ||
         c->ctrl.ensure(4 * sizeof(int32_t)) != hipSuccess) {
         knn_destroy(c);
         return KNN_EHIP;
@@ -820,7 +833,7 @@ knn_status validate_call(knn_ctx* c, const knn_dataset* tr, const knn_dataset* t
 knn_status predict_enqueue(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, int32_t k, int32_t C,
                            const QueryOut& out, hipStream_t st, int algo, int32_t* ctrl_copy) {
     knn_status s;
-    HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st));
+    HIP_OR_FAIL(c, reset_ctrl(c, st));
     if (is_gemm(algo)) {
         // AUTO on fp32 data runs the rounded filter first; when more than 1/16 of the queries
         // (at least 256) overflow its candidate lists, the call is re-run with the split
@@ -992,7 +1005,7 @@ knn_status knn_merge_vote_append(knn_ctx* c, int32_t nsrc, int64_t nq, int32_t k
     HIP_OR_FAIL(c, hipSetDevice(c->device));
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
     if (nq == 0) return KNN_OK;
-    HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st));
+    HIP_OR_FAIL(c, reset_ctrl(c, st));
     MergeArgs m{};
     m.rec = d_rec; m.nsrc = nsrc; m.nq = nq; m.k = k; m.C = C;
     m.out = QueryOut{d_pred, d_dist, d_idx, nullptr, k, 0};
@@ -1186,7 +1199,7 @@ knn_status knn_confusion_matrix_device(knn_ctx* c, const int32_t* d_pred, const 
     HIP_OR_FAIL(c, hipSetDevice(c->device));
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
     c->stages.clear();
-    HIP_OR_FAIL(c, hipMemsetAsync(c->ctrl.p, 0, 4 * sizeof(int32_t), st));
+    HIP_OR_FAIL(c, reset_ctrl(c, st));
     HIP_OR_FAIL(c, hipMemsetAsync(d_cm, 0, sizeof(int32_t) * (size_t)C * (size_t)C, st));
     unsigned long long* corr = reinterpret_cast<unsigned long long*>(d_correct);
     if (!corr) {

@@ -2006,6 +2006,23 @@ __global__ void k_rerun_decide(int32_t* ctrl, int64_t limit) {
     if (open) ctrl[1] = 0;
 }
 
+// The end of a call: the status words go straight to the host's mapped (fine-grained) copy and
+// are reset for the next call -- one tiny kernel instead of a device-to-host copy (a DMA-engine
+// round trip) plus the next call's memset of the words.
+__global__ __launch_bounds__(64) void k_finish(int32_t* __restrict__ ctrl, int32_t* __restrict__ host, int n) {
+    const int i = threadIdx.x;
+    if (i < n) {
+        host[i] = ctrl[i];
+        ctrl[i] = 0;
+    }
+}
+
+hipError_t knn_launch_finish(int32_t* ctrl, int32_t* host_mapped, int n, hipStream_t st) {
+    hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, st, ctrl, host_mapped, n);
+    KNN_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 hipError_t knn_launch_fill_u32(uint32_t* p, int64_t n, uint32_t v, const int32_t* gate, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
