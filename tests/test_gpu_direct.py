@@ -154,3 +154,52 @@ def test_device_dataset_validation(knn):
             ctx.predict_device(wide[:, ::2], lab, test[:, ::2], 5, 10, pred_v)
     finally:
         ctx.close()
+
+
+# k_direct_rows (d <= 16, k <= 16): every feature-group count NG = 1..4 with every remainder,
+# ragged query counts (query groups of 4), train sets shorter than a tile, forced segments
+ROWS_CASES = [(1, 1, 700, 9), (2, 5, 3000, 33), (3, 16, 5000, 7), (4, 2, 63, 5), (5, 3, 65, 13),
+              (6, 7, 9000, 64), (7, 16, 2000, 3), (8, 4, 4100, 101), (9, 9, 130, 40), (10, 1, 8000, 1),
+              (11, 5, 30803 // 4, 1718 // 8), (12, 12, 6000, 66), (13, 6, 129, 17), (14, 15, 7000, 50),
+              (15, 8, 3333, 31), (16, 16, 16, 4)]
+
+
+@pytest.mark.parametrize("d,k,nt,nq", ROWS_CASES)
+def test_direct_rows_vs_oracle(knn, oracle, d, k, nt, nq):
+    """k_direct_rows: per-lane row loads, packed fp32 query pairs (v_pk_add/mul_f32), the sorted
+    first tile and the lane-shift inserts give the oracle's top-k bits and predictions."""
+    tr, tl = oracle.gen(41 + d, 0, 0, nt, d)
+    te, _ = oracle.gen(41 + d, 1, 0, nq, d)
+    ctx = knn.Context(0, algo="direct")
+    try:
+        _check(ctx, oracle, tr, tl, te, min(k, nt), 10)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("splits", [1, 3, 17])
+def test_direct_rows_segments_ties_bf16(knn, oracle, splits):
+    """Forced segments with exact duplicates straddling them (the lower-index tie rule through
+    k_merge_vote), integer-valued features (many equal distances), bf16 rows, subnormal
+    differences, and a class count above the LDS vote table (table-free ballot vote)."""
+    rng = np.random.default_rng(splits)
+    nt, nq, d = 12000, 70, 11
+    tr = rng.integers(-2, 3, size=(nt, d)).astype(np.float32)
+    tr[4000:8000] = tr[:4000]
+    te = rng.integers(-2, 3, size=(nq, d)).astype(np.float32)
+    tl = rng.integers(0, 10, size=nt).astype(np.int32)
+    ctx = knn.Context(0, algo="direct", train_splits=splits)
+    try:
+        for k in (1, 5, 16):
+            st = _check(ctx, oracle, tr, tl, te, k, 10)
+            assert st["train_segments"] == splits
+        sub_tr = (rng.standard_normal((nt, d)) * 2.0 ** -140).astype(np.float32)
+        sub_te = (rng.standard_normal((nq, d)) * 2.0 ** -140).astype(np.float32)
+        _check(ctx, oracle, sub_tr, tl, sub_te, 7, 10)
+        big = rng.integers(0, 3000, size=nt).astype(np.int32)
+        _check(ctx, oracle, tr, big, te, 9, 3000)
+        btr, bl = oracle.gen(47, 0, 0, nt, 16, kind=1)
+        bte, _ = oracle.gen(47, 1, 0, nq, 16, kind=1)
+        _check(ctx, oracle, knn.to_bf16_bits(btr), bl, knn.to_bf16_bits(bte), 10, 10, feats=(btr, bte))
+    finally:
+        ctx.close()
