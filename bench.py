@@ -196,8 +196,10 @@ def oracle_bit_match(seed, kind, nt, d, k, C, q_rows, got_pred, threads=None, ch
         del tr, tl
     want = np.array([int(np.argmax(np.bincount(best_l[q], minlength=C))) for q in range(nq)], np.int32)
     got = np.asarray(got_pred, np.int32)
+    bad = np.nonzero(got != want)[0]
     return {"predictions_equal_oracle": bool(np.array_equal(got, want)), "queries_checked": int(nq),
-            "mismatches": int((got != want).sum()), "query_rows": [int(q) for q in q_rows[:4]] + ["..."],
+            "mismatches": int(len(bad)), "mismatch_rows": [int(q_rows[i]) for i in bad[:8]],
+            "query_rows": [int(q) for q in q_rows[:4]] + ["..."],
             "checker": "oracle/knn_oracle.c over the whole train set (host-regenerated, chunked, merged)",
             "check_s": round(time.perf_counter() - t0, 1)}
 

@@ -295,16 +295,29 @@ knn_status knn_predict_train_sharded(knn_ctx* ctx, knn_comm* comm, const knn_dat
     int64_t so[1024], sc[1024], ro[1024], rc[1024];
     knn_exchange_layout(nq, k, comm->nranks, comm->rank, so, sc, ro, rc);
     knn_ctx_stage_begin(ctx, st, "exchange");
-    if (r.group_start() != ncclSuccess) return give_up();
-    bool ok = true;
-    for (int32_t b = 0; b < comm->nranks && ok; b++) {
-        if (sc[b] > 0 && r.send((const int32_t*)comm->rec + so[b], (size_t)sc[b], ncclInt32, b, comm->comm, st) != ncclSuccess)
-            ok = false;
-        if (ok && rc[b] > 0 &&
-            r.recv((int32_t*)comm->lists + ro[b], (size_t)rc[b], ncclInt32, b, comm->comm, st) != ncclSuccess)
-            ok = false;
+    // this rank's own block is a device copy; the peers' blocks go through RCCL in pieces of at
+    // most KNN_XCHG_CHUNK elements.  (Round 5: a one-rank communicator's grouped self send/recv of
+    // config C1's 1.2 GB of records delivered only its first half -- the queries past ~500k got
+    // wrong neighbour lists, r05i -- so no transfer relies on a single multi-GB RCCL message.)
+    constexpr size_t KNN_XCHG_CHUNK = (size_t)64 << 20;  // 256 MiB of int32 per send / recv
+    if (sc[comm->rank] > 0 &&
+        hipMemcpyAsync((int32_t*)comm->lists + ro[comm->rank], (const int32_t*)comm->rec + so[comm->rank],
+                       sizeof(int32_t) * (size_t)sc[comm->rank], hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return give_up();  // (every rank takes this branch alike; a failure here is local -- see give_up)
+    if (comm->nranks > 1) {
+        if (r.group_start() != ncclSuccess) return give_up();
+        bool ok = true;
+        for (int32_t b = 0; b < comm->nranks && ok; b++) {
+            if (b == comm->rank) continue;
+            for (int64_t o = 0; ok && o < sc[b]; o += (int64_t)KNN_XCHG_CHUNK)
+                ok = r.send((const int32_t*)comm->rec + so[b] + o, (size_t)std::min<int64_t>(KNN_XCHG_CHUNK, sc[b] - o),
+                            ncclInt32, b, comm->comm, st) == ncclSuccess;
+            for (int64_t o = 0; ok && o < rc[b]; o += (int64_t)KNN_XCHG_CHUNK)
+                ok = r.recv((int32_t*)comm->lists + ro[b] + o, (size_t)std::min<int64_t>(KNN_XCHG_CHUNK, rc[b] - o),
+                            ncclInt32, b, comm->comm, st) == ncclSuccess;
+        }
+        if (r.group_end() != ncclSuccess || !ok) return give_up();
     }
-    if (r.group_end() != ncclSuccess || !ok) return give_up();
     knn_ctx_stage_end(ctx, st);
     // 4. merge + vote of the owned queries (ordered by distance, then global index); the
     //    shard's stage times stay in the context's profile beside the exchange and the merge

@@ -212,3 +212,38 @@ def test_rccl_train_sharded_single_rank(knn, oracle, dtype, d, k, nt, nq):
     finally:
         comm.close()
         ctx.close()
+
+
+def test_train_sharded_c_abi_large_exchange(knn):
+    """knn_predict_train_sharded with records past 2^30 bytes (700k queries x k = 100: 840 MB):
+    round 5 found a one-rank communicator's single RCCL self send/recv of config C1's 1.2 GB
+    delivering only its first half (queries past ~500k wrong).  The C-ABI path must equal the
+    shard top-k + merge path on every query: predictions, neighbour indices and distance bits."""
+    import torch
+    nt, nq, d, k = 20_000, 700_000, 64, 100
+    dev = "cuda:0"
+    ctx = knn.Context(0)
+    train = torch.empty((nt, d), dtype=torch.bfloat16, device=dev)
+    labels = torch.empty(nt, dtype=torch.int32, device=dev)
+    test = torch.empty((nq, d), dtype=torch.bfloat16, device=dev)
+    ctx.generate(train, labels, 0, d, 1, 37, 0, 10)
+    ctx.generate(test, None, 0, d, 1, 37, 1, 10)
+    comm = knn.Comm(ctx, knn.comm_unique_id(), 1, 0)
+    try:
+        pred = torch.empty(nq, dtype=torch.int32, device=dev)
+        dist = torch.empty((nq, k), dtype=torch.float32, device=dev)
+        idx = torch.empty((nq, k), dtype=torch.int32, device=dev)
+        comm.predict_train_sharded(train, labels, 0, test, k, 10, pred, dist, idx)
+        rec = torch.empty((nq, 3, k), dtype=torch.int32, device=dev)
+        ctx.shard_topk_device(train, labels, test, k, 10, 0, rec)
+        pred2 = torch.empty(nq, dtype=torch.int32, device=dev)
+        dist2 = torch.empty((nq, k), dtype=torch.float32, device=dev)
+        idx2 = torch.empty((nq, k), dtype=torch.int32, device=dev)
+        ctx.merge_vote_device(rec.view(1, nq, 3, k), k, 10, pred2, dist2, idx2)
+        torch.cuda.synchronize()
+        assert torch.equal(idx, idx2)
+        assert torch.equal(dist.view(torch.int32), dist2.view(torch.int32))
+        assert torch.equal(pred, pred2)
+    finally:
+        comm.close()
+        ctx.close()
