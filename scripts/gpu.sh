@@ -66,7 +66,7 @@ for cfg in $BENCHES; do
 done
 
 for cfg in $PROFILE; do
-  st=2; [ "$cfg" != A ] && st=1
+  st=2; [ "$cfg" != A ] && st=1; [ "$cfg" = L ] && st=50
   STEPS=$st PROF_TAG=${TAG}_$cfg BENCH_ARGS="--config $cfg ${PROFILE_ARGS:-}" bash scripts/profile_bench.sh || exit 1
 done
 
