@@ -38,6 +38,7 @@ import json
 import os
 import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -341,6 +342,75 @@ def pmc_traffic(key):
     return rec.get("gemm_filter_bytes_per_launch"), rec.get("tag")
 
 
+XCHECK_LIMIT_S = 180  # the exchange check's watchdog (a hung collective ends the run, line printed)
+
+
+def rccl_exchange_check(knn, torch, dist, local, world, rank, share, seed):
+    """The C-ABI train-sharded path over a real multi-rank RCCL communicator, checked: every rank
+    holds shard_range(NT, world, rank) of a small synthetic train set and all NQ queries,
+    knn_predict_train_sharded (shard top-k -> grouped ncclSend/Recv -> merge + vote) gives the
+    owned queries' neighbour lists, and the same queries against the WHOLE train set on the
+    rank's own GPU (knn_predict_device, the test-sharded path the parity suite pins to the
+    oracle) must give the same predictions, global indices and distance bits (mpi.cpp:173-186:
+    the gather the exchange replaces).  Runs after the timed region of a multi-rank line, so the
+    driver's N = 2/4/8 runs exercise the exchange on xGMI; returns the summary for the line."""
+    nt_s, nq_s, d_s, k_s, c_s = 262_144, 8_192, 64, 16, 10
+    out = {"n_train": nt_s, "n_query": nq_s, "d": d_s, "k": k_s, "ranks": world, "status": "ok"}
+    dev = torch.device("cuda", local)
+    bad, ok = 0, 1
+    t0 = time.perf_counter()
+    ctx = comm = None
+    try:
+        ctx = knn.Context(local, profile=3)
+        uid = [knn.comm_unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        comm = knn.Comm(ctx, uid[0], world, rank)
+        out["rccl_comm_ranks"] = comm.count()
+        a0, a1 = knn.shard_range(nt_s, world, rank)
+        m0, m1 = knn.shard_range(nq_s, world, rank)
+        shard = torch.empty((a1 - a0, d_s), dtype=torch.float32, device=dev)
+        slab = torch.empty(a1 - a0, dtype=torch.int32, device=dev)
+        test = torch.empty((nq_s, d_s), dtype=torch.float32, device=dev)
+        ctx.generate(shard, slab, a0, d_s, 0, seed, 0, c_s)
+        ctx.generate(test, None, 0, d_s, 0, seed, 1, c_s)
+        pred = torch.empty(m1 - m0, dtype=torch.int32, device=dev)
+        dd = torch.empty((m1 - m0, k_s), dtype=torch.float32, device=dev)
+        ii = torch.empty((m1 - m0, k_s), dtype=torch.int32, device=dev)
+        comm.predict_train_sharded(shard, slab, a0, test, k_s, c_s, pred, dist=dd, idx=ii)
+        torch.cuda.synchronize(dev)
+        out["exchange_ms"] = round(ctx.stage_times().get("exchange", float("nan")), 3)
+        full = torch.empty((nt_s, d_s), dtype=torch.float32, device=dev)
+        flab = torch.empty(nt_s, dtype=torch.int32, device=dev)
+        ctx.generate(full, flab, 0, d_s, 0, seed, 0, c_s)
+        rp = torch.empty_like(pred)
+        rd = torch.empty_like(dd)
+        ri = torch.empty_like(ii)
+        if m1 > m0:
+            ctx.predict_device(full, flab, test[m0:m1], k_s, c_s, rp, dist=rd, idx=ri)
+        torch.cuda.synchronize(dev)
+        rows = (pred != rp) | (ii != ri).any(dim=1) | (dd.view(torch.int32) != rd.view(torch.int32)).any(dim=1)
+        bad = int(rows.sum().item())
+    except Exception as e:  # reported on the line; the ranks still meet at the all-reduce below
+        ok = 0
+        out["status"] = "error"
+        out["error"] = f"rank {rank}: {e!r}"[:300]
+    finally:
+        if comm is not None:
+            comm.close()
+        if ctx is not None:
+            ctx.close()
+    v = torch.tensor([bad, 1 - ok], dtype=torch.int64, device="cpu" if share else dev)
+    if world > 1:
+        dist.all_reduce(v)
+    out["mismatched_queries"] = int(v[0].item())
+    if int(v[1].item()) and out["status"] == "ok":
+        out["status"] = "error on another rank"
+    out["equal_to_whole_train_path"] = out["status"] == "ok" and out["mismatched_queries"] == 0
+    out["check_s"] = round(time.perf_counter() - t0, 2)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -578,6 +648,7 @@ def main():
         if rank == 0:
             gathered = int((full >= 0).sum())
 
+    line = None
     if rank == 0:
         pairs = float(total_q) * nt * args.steps
         stages = {n: v / args.steps for n, v in stage_sum.items()}
@@ -643,7 +714,25 @@ def main():
             "select_stage": select,
             "host_buffers": host,
         }
-        print(json.dumps(out), flush=True)
+        line = out
+    # multi-rank lines: the train-sharded C-ABI path over a real RCCL communicator of all ranks,
+    # checked against the whole-train path (KNN_BENCH_XCHECK=1 runs it at one rank too)
+    if (world > 1 and not share) or os.environ.get("KNN_BENCH_XCHECK") == "1":
+        def expired():
+            if line is not None:
+                line["rccl_exchange_check"] = {"status": "timeout", "limit_s": XCHECK_LIMIT_S}
+                print(json.dumps(line), flush=True)
+            print(f"[bench rank {rank}] exchange check timed out", file=sys.stderr, flush=True)
+            os._exit(0)
+        wd = threading.Timer(XCHECK_LIMIT_S, expired)
+        wd.daemon = True
+        wd.start()
+        xc = rccl_exchange_check(knn, torch, dist, local, world, rank, share, seed)
+        wd.cancel()
+        if line is not None:
+            line["rccl_exchange_check"] = xc
+    if line is not None:
+        print(json.dumps(line), flush=True)
     if comm is not None:
         comm.close()
     ctx.close()

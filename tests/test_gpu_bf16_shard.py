@@ -247,3 +247,22 @@ def test_train_sharded_c_abi_large_exchange(knn):
     finally:
         comm.close()
         ctx.close()
+
+
+def test_bench_exchange_check_single_rank(knn):
+    """bench.py's rccl_exchange_check -- what the driver's N = 2/4/8 lines run after their timed
+    region -- at one rank: the train-sharded C-ABI path over an RCCL communicator must equal
+    the whole-train path query for query (predictions, indices, distance bits)."""
+    import importlib.util
+    import os
+
+    import torch
+    import torch.distributed as dist
+    spec = importlib.util.spec_from_file_location(
+        "bench_mod", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    out = bench.rccl_exchange_check(knn, torch, dist, 0, 1, 0, False, 7)
+    assert out["status"] == "ok", out
+    assert out["rccl_comm_ranks"] == 1
+    assert out["mismatched_queries"] == 0 and out["equal_to_whole_train_path"], out
