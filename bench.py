@@ -120,8 +120,8 @@ def cpu_baseline(d, k, C, seed, kind=0, nt_cfg=1_000_000):
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from conftest import Oracle
     o = Oracle()
-    tr, tl = o.gen(seed, 0, 0, nt_s, d, kind=kind)
-    te, _ = o.gen(seed, 1, 0, nq_s, d, kind=kind)
+    tr, tl = o.gen(seed, 0, 0, nt_s, d, kind=kind, C=C)
+    te, _ = o.gen(seed, 1, 0, nq_s, d, kind=kind, C=C)
     t0 = time.perf_counter()
     o.knn(tr, tl, te, k, C, threads=threads, topk=False)
     dt = time.perf_counter() - t0
@@ -438,6 +438,9 @@ def main():
                          "exchange + merge) or auto (knn_shard_policy); default: the config's own")
     ap.add_argument("--no-uncached", action="store_true",
                     help="skip the extra steps that time a context without the train-operand cache")
+    ap.add_argument("--data", default="uniform", choices=["uniform", "clustered"],
+                    help="synthetic rows: uniform (SURVEY.md 8d, labels independent of the rows) or "
+                         "clustered (class centroid + noise: the labels carry signal, accuracy is non-trivial)")
     ap.add_argument("--no-bit-match", action="store_true",
                     help="skip the oracle check of a sample of this run's predictions")
     args = ap.parse_args()
@@ -489,6 +492,8 @@ def main():
     else:
         scaling = "strong"
     kind = 1 if dtype == "bf16" else 0                  # bf16-exact generator values for bf16
+    if args.data == "clustered":
+        kind += 2                                       # the clustered variants (kinds 2 / 3)
     tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
     dev = torch.device("cuda", local)
     # the train set is resident and unchanged across steps (a serving process): the context
@@ -511,7 +516,8 @@ def main():
     labels = torch.empty(nt_local, dtype=torch.int32, device=dev)
     test = torch.empty((nq, d), dtype=tdt, device=dev)
     ctx.generate(train, labels, t0_row, d, kind, seed, 0, C)
-    ctx.generate(test, None, q0, d, kind, seed, 1, C)
+    truth = torch.empty(nq, dtype=torch.int32, device=dev)  # the generator's labels of the query rows
+    ctx.generate(test, truth, q0, d, kind, seed, 1, C)
     if sharding == "test":
         pred = torch.empty(nq, dtype=torch.int32, device=dev)
     else:
@@ -637,6 +643,10 @@ def main():
         n_s = 64 if float(nt) * d <= 2.1e9 else 8
         pos = np.unique(np.linspace(0, len(pl) - 1, min(n_s, len(pl))).astype(np.int64))
         bitm = oracle_bit_match(seed, kind, nt, d, k, C, own_q0 + pos, pl[pos])
+    # computeAccuracy (main.cpp:102-112) of this rank's predictions against the generator's labels
+    # of its query rows (~1/C for uniform rows, whose labels carry no signal)
+    own_truth = truth if sharding == "test" else truth[own0:own1]
+    accuracy = round(float((pred_timed == own_truth).float().mean().item()), 6) if len(pred_timed) else None
     host = None
     if rank == 0 and world == 1 and sharding == "test" and not args.no_host_path:
         host = host_buffer_times(knn, local, args.algo, train, labels, test, k, C, pred)
@@ -657,6 +667,7 @@ def main():
         operands = stats.get("filter_operands") or dtype
         # the workload key of the PMC summaries (scripts/summarize_profile.py reads it back)
         pmc_key = (args.config + ("" if operands == dtype else PMC_SUFFIX.get(operands, "/" + operands))
+                   + ("/clustered" if args.data == "clustered" else "")
                    + (f"/nt{args.nt}" if args.nt else "") + (f"/nq{args.nq}" if args.nq else ""))
         roof = None
         if filt_ms:
@@ -690,8 +701,11 @@ def main():
             "metric": METRIC, "value": pairs / elapsed, "unit": "pairs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": dtype,
-            "data": "synthetic (counter-based generator, SURVEY.md 8d), generated in HBM",
-            "config": {"workload": f"{args.config}: synthetic {nt} train x {nq_cfg} query"
+            "data": (f"synthetic{' clustered (class centroid + noise)' if args.data == 'clustered' else ''} "
+                     "(counter-based generator, SURVEY.md 8d), generated in HBM"),
+            "accuracy_vs_generator_labels": accuracy,
+            "config": {"workload": f"{args.config}: synthetic{' clustered' if args.data == 'clustered' else ''} "
+                                   f"{nt} train x {nq_cfg} query"
                                    f"{'/GPU' if scaling == 'weak' else ''} x {d}-d {dtype}, k={k}",
                        "n_train": nt, "n_query_total": total_q, "d": d, "k": k, "classes": C,
                        "parallelism": par, "shard": {"requested": shard_req, "used": sharding}},

@@ -267,7 +267,9 @@ int32_t knn_last_stats(const knn_ctx* ctx, int64_t* out, int32_t n);
  * Synthetic generator, device side: fills rows [row0, row0+n) of a
  * row-major [n][ld] device buffer (pad columns zeroed) and optional labels,
  * from the counter-based hash keyed by (seed, stream, row, col).
- * kind: 0 = fp32 on the 2^-23 grid in [-1,1), 1 = bf16-exact k/128.
+ * kind: 0 = fp32 on the 2^-23 grid in [-1,1), 1 = bf16-exact k/128; 2 / 3 = the same two
+ *       clustered: the row's class centroid + noise, so labels carry signal
+ *       (needs num_classes >= 1; bf16 output: kinds 1 and 3).
  * out dtype follows `dtype` (KNN_BF16 stores bf16 bits).
  */
 knn_status knn_generate(knn_ctx* ctx, void* d_feat, int32_t* d_labels, int64_t row0, int64_t n,

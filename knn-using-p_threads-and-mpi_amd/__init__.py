@@ -441,7 +441,9 @@ class Context:
     def generate(self, feat, labels, row0, d, kind, seed, stream_id, num_classes, dtype=None,
                  stream=None):
         """Fill a device tensor [n][ld] (and labels) with the synthetic rows of SURVEY.md 8d.
-        A bfloat16 tensor receives bf16 bits (kind 1 only: bf16-exact values)."""
+        kind 0 / 1: uniform fp32 grid / bf16-exact values; 2 / 3: the same clustered (the row's
+        class centroid + noise: labels carry signal).  A bfloat16 tensor receives bf16 bits
+        (kinds 1 and 3: bf16-exact values)."""
         dtype = _tensor_dtype(feat) if dtype is None else dtype
         self._check(self.lib.knn_generate(
             self.h, feat.data_ptr(), None if labels is None else labels.data_ptr(), row0,

@@ -1166,10 +1166,12 @@ knn_status knn_generate(knn_ctx* c, void* d_feat, int32_t* d_labels, int64_t row
                         int32_t ld, int32_t dtype, int32_t kind, uint64_t seed, uint32_t stream,
                         int32_t C, void* hip_stream) {
     if (!c) return KNN_EINVAL;
-    if (n < 0 || d <= 0 || ld < d || (d_labels && C < 1) || (n > 0 && !d_feat) || (kind != 0 && kind != 1) ||
+    if (n < 0 || d <= 0 || ld < d || (d_labels && C < 1) || (n > 0 && !d_feat) || kind < 0 || kind > 3 ||
         (dtype != KNN_F32 && dtype != KNN_BF16))
         return fail(c, KNN_EINVAL, "knn_generate: bad arguments");
-    if (dtype == KNN_BF16 && kind != 1) return fail(c, KNN_EINVAL, "bf16 output needs kind=1 (bf16-exact values)");
+    if (dtype == KNN_BF16 && kind != 1 && kind != 3)
+        return fail(c, KNN_EINVAL, "bf16 output needs kind 1 or 3 (bf16-exact values)");
+    if (kind >= 2 && C < 1) return fail(c, KNN_EINVAL, "clustered kinds need num_classes >= 1");
     HIP_OR_FAIL(c, hipSetDevice(c->device));
     GenerateArgs a{d_feat, d_labels, row0, n, d, ld, dtype == KNN_BF16, kind, seed, stream, C};
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;

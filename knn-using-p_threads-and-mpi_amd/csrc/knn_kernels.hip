@@ -1928,6 +1928,11 @@ __device__ __forceinline__ uint64_t gen_hash(uint64_t seed, uint32_t stream, uin
     return mix64(x);
 }
 
+// kinds 2 / 3 (SURVEY.md 8d's clustered variant): the class centroids' stream, as in
+// oracle/knn_oracle.c
+#define GEN_CENTROID_STREAM 0xC3u
+__device__ __forceinline__ float grid_value(uint32_t u) { return (float)(int32_t)(u >> 8) * (1.0f / 8388608.0f) - 1.0f; }
+
 __global__ __launch_bounds__(256) void k_generate(GenerateArgs a) {
     const int64_t total = a.n * a.ld;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total || i < a.n; i += (int64_t)gridDim.x * 256) {
@@ -1936,12 +1941,26 @@ __global__ __launch_bounds__(256) void k_generate(GenerateArgs a) {
         int c = (int)(i % a.ld);
         float v = 0.0f;
         if (c < a.d) {
-            uint32_t u = (uint32_t)(gen_hash(a.seed, a.stream, (uint64_t)(a.row0 + r), (uint32_t)c) >> 32);
-            v = (a.kind == 1) ? (float)((int32_t)(u >> 24) - 128) * (1.0f / 128.0f)
-                              : (float)(int32_t)(u >> 8) * (1.0f / 8388608.0f) - 1.0f;
+            const uint64_t row = (uint64_t)(a.row0 + r);
+            uint32_t u = (uint32_t)(gen_hash(a.seed, a.stream, row, (uint32_t)c) >> 32);
+            if (a.kind == 1) {
+                v = (float)((int32_t)(u >> 24) - 128) * (1.0f / 128.0f);
+            } else if (a.kind >= 2) {
+                // clustered: the row's class centroid (stream GEN_CENTROID_STREAM, row = class)
+                // plus noise -- kind 2: grid centroid + 0.5 x grid value (exact product, one
+                // rounded add, no contraction: pragma below); kind 3: bf16-exact (k1 + k2)/128
+                const uint32_t cls = (uint32_t)(gen_hash(a.seed, a.stream, row, 0xFFFFu) >> 32) % (uint32_t)a.C;
+                const uint32_t m = (uint32_t)(gen_hash(a.seed, GEN_CENTROID_STREAM, cls, (uint32_t)c) >> 32);
+                if (a.kind == 3)
+                    v = (float)(((int32_t)(m >> 24) - 128) + ((int32_t)(u >> 26) - 32)) * (1.0f / 128.0f);
+                else
+                    v = grid_value(m) + 0.5f * grid_value(u);
+            } else {
+                v = grid_value(u);
+            }
         }
         if (a.bf16_out)
-            reinterpret_cast<uint16_t*>(a.out)[i] = (uint16_t)(__float_as_uint(v) >> 16);  // exact for kind 1
+            reinterpret_cast<uint16_t*>(a.out)[i] = (uint16_t)(__float_as_uint(v) >> 16);  // exact for kinds 1, 3
         else
             reinterpret_cast<float*>(a.out)[i] = v;
     }

@@ -195,19 +195,42 @@ uint64_t oracle_hash(uint64_t seed, uint32_t stream, uint64_t row, uint32_t col)
     return mix64(x);
 }
 
-/* kind 0: fp32 on the 2^-23 grid in [-1, 1); kind 1: bf16-exact k/128, k in [-128, 128). */
-float oracle_gen_value(uint64_t seed, uint32_t stream, uint64_t row, uint32_t col, int kind)
-{
-    uint32_t u = (uint32_t)(oracle_hash(seed, stream, row, col) >> 32);
-    if (kind == 1) return (float)((int32_t)(u >> 24) - 128) * (1.0f / 128.0f);
-    return (float)(int32_t)(u >> 8) * (1.0f / 8388608.0f) - 1.0f;
-}
-
+/* kind 0: fp32 on the 2^-23 grid in [-1, 1); kind 1: bf16-exact k/128, k in [-128, 128).
+ * Clustered kinds (SURVEY.md 8d's "clustered" variant, labels that carry signal): the row's
+ * label picks a class centroid (the same hash on stream ORACLE_CENTROID_STREAM, row = class)
+ * and the value is centroid + noise.  kind 2: centroid on the 2^-23 grid in [-1, 1) plus half
+ * a grid value in [-1, 1) (the product 0.5 n is exact, so the one fp32 add rounds the same
+ * anywhere); kind 3: bf16-exact (k1 + k2)/128, k1 in [-128, 128), k2 in [-32, 32): |k1 + k2|
+ * <= 160 is an integer a bf16 holds exactly. */
 #define ORACLE_LABEL_COL 0xFFFFu
+#define ORACLE_CENTROID_STREAM 0xC3u
 int32_t oracle_gen_label(uint64_t seed, uint32_t stream, uint64_t row, int C)
 {
     uint32_t u = (uint32_t)(oracle_hash(seed, stream, row, ORACLE_LABEL_COL) >> 32);
     return (int32_t)(u % (uint32_t)C);
+}
+
+static float grid_value(uint32_t u) { return (float)(int32_t)(u >> 8) * (1.0f / 8388608.0f) - 1.0f; }
+
+float oracle_gen_value_c(uint64_t seed, uint32_t stream, uint64_t row, uint32_t col, int kind, int C)
+{
+    uint32_t u = (uint32_t)(oracle_hash(seed, stream, row, col) >> 32);
+    if (kind == 1) return (float)((int32_t)(u >> 24) - 128) * (1.0f / 128.0f);
+    if (kind == 2 || kind == 3) {
+        const int32_t cls = oracle_gen_label(seed, stream, row, C);
+        uint32_t m = (uint32_t)(oracle_hash(seed, ORACLE_CENTROID_STREAM, (uint64_t)cls, col) >> 32);
+        if (kind == 3)
+            return (float)(((int32_t)(m >> 24) - 128) + ((int32_t)(u >> 26) - 32)) * (1.0f / 128.0f);
+        volatile float noise = 0.5f * grid_value(u); /* exact; kept apart from the add */
+        return grid_value(m) + noise;
+    }
+    return grid_value(u);
+}
+
+/* the unclustered kinds (0, 1) need no class count */
+float oracle_gen_value(uint64_t seed, uint32_t stream, uint64_t row, uint32_t col, int kind)
+{
+    return oracle_gen_value_c(seed, stream, row, col, kind, 10);
 }
 
 /* Fill rows [row0, row0+n) of a row-major [n][ld] block (pad columns = 0). */
@@ -216,7 +239,7 @@ void oracle_gen_block(uint64_t seed, uint32_t stream, int64_t row0, int64_t n, i
 {
     for (int64_t r = 0; r < n; r++) {
         for (int c = 0; c < d; c++)
-            out[r * ld + c] = oracle_gen_value(seed, stream, (uint64_t)(row0 + r), (uint32_t)c, kind);
+            out[r * ld + c] = oracle_gen_value_c(seed, stream, (uint64_t)(row0 + r), (uint32_t)c, kind, C);
         for (int64_t c = d; c < ld; c++) out[r * ld + c] = 0.0f;
         if (labels) labels[r] = oracle_gen_label(seed, stream, (uint64_t)(row0 + r), C);
     }

@@ -13,7 +13,7 @@
 // (oracle/knn_oracle.c oracle_gen_*), so the predictions can be cross-checked.
 //
 // usage: ref_bench kind seed nt nq d k C threads [pred_out]
-//   kind 0 = fp32 grid values, 1 = bf16-exact values
+//   kind 0 = fp32 grid values, 1 = bf16-exact values, 2 / 3 = their clustered variants
 // stdout: one JSON line {"ms":..,"pairs_per_s":..,"queries_per_s":..,"threads":..}
 #define main reference_main
 #include REF_MT_CPP
@@ -22,7 +22,7 @@
 #include <string>
 
 extern "C" {
-float oracle_gen_value(uint64_t seed, uint32_t stream, uint64_t row, uint32_t col, int kind);
+float oracle_gen_value_c(uint64_t seed, uint32_t stream, uint64_t row, uint32_t col, int kind, int C);
 int32_t oracle_gen_label(uint64_t seed, uint32_t stream, uint64_t row, int C);
 }
 
@@ -33,7 +33,7 @@ static ArffData* build(int kind, uint64_t seed, uint32_t stream, long n, int d, 
     for (long r = 0; r < n; r++) {
         ArffInstance* inst = new ArffInstance();
         for (int c = 0; c < d; c++)
-            inst->add(new ArffValue(oracle_gen_value(seed, stream, (uint64_t)r, (uint32_t)c, kind)));
+            inst->add(new ArffValue(oracle_gen_value_c(seed, stream, (uint64_t)r, (uint32_t)c, kind, C)));
         inst->add(new ArffValue((float)oracle_gen_label(seed, stream, (uint64_t)r, C)));
         data->add_instance(inst);
     }

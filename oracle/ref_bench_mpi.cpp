@@ -19,7 +19,7 @@
 #include <string>
 
 extern "C" {
-float oracle_gen_value(uint64_t seed, uint32_t stream, uint64_t row, uint32_t col, int kind);
+float oracle_gen_value_c(uint64_t seed, uint32_t stream, uint64_t row, uint32_t col, int kind, int C);
 int32_t oracle_gen_label(uint64_t seed, uint32_t stream, uint64_t row, int C);
 }
 
@@ -30,7 +30,7 @@ static ArffData* build(int kind, uint64_t seed, uint32_t stream, long n, int d, 
     for (long r = 0; r < n; r++) {
         ArffInstance* inst = new ArffInstance();
         for (int c = 0; c < d; c++)
-            inst->add(new ArffValue(oracle_gen_value(seed, stream, (uint64_t)r, (uint32_t)c, kind)));
+            inst->add(new ArffValue(oracle_gen_value_c(seed, stream, (uint64_t)r, (uint32_t)c, kind, C)));
         inst->add(new ArffValue((float)oracle_gen_label(seed, stream, (uint64_t)r, C)));
         data->add_instance(inst);
     }

@@ -292,7 +292,7 @@ def test_edge_cases(knn, ctxs):
 def test_generator_matches_oracle(knn, oracle):
     import torch
     c = knn.Context(0)
-    for kind, d, ld in ((0, 128, 128), (0, 11, 16), (1, 256, 256)):
+    for kind, d, ld in ((0, 128, 128), (0, 11, 16), (1, 256, 256), (2, 128, 128), (2, 11, 16), (3, 64, 64)):
         feat = torch.empty((777, ld), dtype=torch.float32, device="cuda:0")
         lab = torch.empty(777, dtype=torch.int32, device="cuda:0")
         c.generate(feat, lab, 1000, d, kind, 5, 1, 10)

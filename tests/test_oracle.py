@@ -97,6 +97,25 @@ def test_oracle_generator_values(oracle):
     assert np.all(fb * 128 == np.round(fb * 128)) and fb.min() >= -1 and fb.max() < 1
 
 
+def test_oracle_clustered_generator(oracle):
+    """SURVEY.md 8d's clustered variant (kinds 2 / 3): value = the row's class centroid +
+    noise, exact on its grid, rows independent of the block, and labels that carry signal."""
+    f, lab = oracle.gen(4, 0, 0, 400, 64, kind=2)
+    g = f.astype(np.float64) * 2 ** 24  # centroid (2^-23 grid) + half a grid value: 2^-24 grid
+    assert np.all(g == np.round(g)) and np.abs(f).max() < 1.5
+    f2, _ = oracle.gen(4, 0, 200, 200, 64, kind=2)
+    assert np.array_equal(f[200:], f2)
+    t, tl = oracle.gen(4, 1, 0, 50, 64, kind=2)  # test rows: same centroids, their own noise
+    _, pred, _, _ = oracle.knn(f, lab, t, 3, 10)
+    assert np.mean(pred == tl) > 0.9  # uniform data gives ~0.1
+    fb, lb = oracle.gen(5, 0, 0, 300, 32, kind=3)
+    assert np.all(fb * 128 == np.round(fb * 128)) and np.abs(fb * 128).max() <= 160
+    # bf16-exact: the top 16 bits hold the whole value
+    assert np.array_equal(fb.view(np.uint32) & 0xFFFF, np.zeros_like(fb.view(np.uint32)))
+    # kinds 0 / 1 unchanged by the class count
+    assert np.array_equal(oracle.gen(1, 0, 0, 8, 16, kind=0, C=3)[0], oracle.gen(1, 0, 0, 8, 16, kind=0, C=10)[0])
+
+
 def test_oracle_k_above_n_flags(oracle):
     tr = np.zeros((3, 2), np.float32)
     bad, *_ = oracle.knn(tr, np.zeros(3, np.int32), tr, 4, 1)
@@ -130,6 +149,23 @@ def test_reference_mpi_bench_matches_pthreads_and_oracle(oracle, tmp_path):
     te, _ = oracle.gen(7, 1, 0, 61, 32)
     _, opred, _, _ = oracle.knn(tr, tl, te, 5, 10)
     assert np.array_equal(mpi, opred) and np.array_equal(mt, opred)
+
+
+def test_reference_clustered_matches_oracle(oracle, tmp_path):
+    """The reference's own pthreads KNN (ref_bench: multi-thread.cpp compiled from
+    /root/reference) on clustered rows (kind 2, built through libarff's API) gives the oracle's
+    predictions: the clustered generator's values are pinned by the reference itself."""
+    import subprocess
+    argv = ["2", "9", "4000", "64", "24", "7", "10"]
+    r = subprocess.run([_ref_mpi("ref_bench")] + argv + ["4", str(tmp_path / "mt.txt")], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    mt = np.loadtxt(tmp_path / "mt.txt", dtype=np.int32)
+    tr, tl = oracle.gen(9, 0, 0, 4000, 24, kind=2)
+    te, truth = oracle.gen(9, 1, 0, 64, 24, kind=2)
+    _, opred, _, _ = oracle.knn(tr, tl, te, 7, 10)
+    assert np.array_equal(mt, opred)
+    assert np.mean(opred == truth) > 0.8
 
 
 def test_reference_mpi_binary_line():
