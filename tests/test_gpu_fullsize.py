@@ -13,7 +13,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _run_full(knn, oracle, nt, nq, d, k, seed, n_sample, expect_segments_min):
+def _run_full(knn, oracle, nt, nq, d, k, seed, n_sample, expect_segments_min, q0=0):
     import torch
     dev = "cuda:0"
     gen = knn.Context(0)
@@ -21,7 +21,7 @@ def _run_full(knn, oracle, nt, nq, d, k, seed, n_sample, expect_segments_min):
     labels = torch.empty(nt, dtype=torch.int32, device=dev)
     test = torch.empty((nq, d), dtype=torch.float32, device=dev)
     gen.generate(train, labels, 0, d, 0, seed, 0, 10)
-    gen.generate(test, None, 0, d, 0, seed, 1, 10)
+    gen.generate(test, None, q0, d, 0, seed, 1, 10)
     gen.close()
     out = {}
     for algo in ("auto", "direct"):
@@ -64,3 +64,16 @@ def test_full_size_config_b(knn, oracle):
     the two-block 4-wave shape for 128-byte bf16 rows, several train segments)."""
     st = _run_full(knn, oracle, 4_000_000, 1_000_000, 64, 32, 2, 16, 2)
     assert st["fallback_queries"] < 1_000_000 // 16, st
+
+
+def test_config_a_rank_share(knn, oracle):
+    """Config A's per-rank share at 8 GPUs under the fixed-problem split (bench --strong): the
+    last rank's 12,500 query rows (knn_rank_queries, mpi.cpp:141-170) against the whole 1M
+    train set -- the partition knn_shard_policy picks for A (test-sharded), in the plan's
+    share-size shape (32 queries per wave, each query tile cut into pieces that exchange
+    thresholds and lists).  Every query bit-exact against the direct form."""
+    q0, nq = knn.rank_queries(100_000, 8, 7, "strong")
+    assert (q0, nq) == (87_500, 12_500)
+    assert knn.shard_policy(1_000_000, 100_000, 128, "f32", 8, 288 << 30) == "test"
+    st = _run_full(knn, oracle, 1_000_000, nq, 128, 10, 1, 24, 1, q0=q0)
+    assert st["fused_norm"], st
