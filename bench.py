@@ -257,7 +257,10 @@ def bench_arff(args, knn, torch, local):
         kernel = ("k_direct_rows" if d <= 16 and k <= 16 else "k_direct_tile") if kname == "direct_tile" \
             else "k_exact_scan"
         roof = {"bound": "valu", "achieved": round(ops / (scan * 1e-3) / 1e12, 3), "peak": 78.6,
-                "unit": "Tops/s", "frac": round(ops / (scan * 1e-3) / 1e12 / 78.6, 4), "traffic": None,
+                "unit": "Tops/s", "frac": round(ops / (scan * 1e-3) / 1e12 / 78.6, 4),
+                "traffic": pmc_traffic("L")[0] if kernel == "k_direct_rows" else None,
+                "traffic_source": (pmc_traffic("L")[1] and f"profiles/{pmc_traffic('L')[1]}_pmc_traffic.json")
+                if kernel == "k_direct_rows" else None,
                 "kernel": kernel, "avg_launch_ms": round(scan, 4),
                 "peak_basis": "fp32 VALU: 256 CUs x 4 SIMDs x 32 lanes/clk at 2.4 GHz, packed fp32 "
                               "(v_pk_add/mul_f32: two ops per lane) -- MI355X_MICROARCH.md: 157.3 TFLOP/s "

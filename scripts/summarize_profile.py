@@ -67,6 +67,8 @@ def main():
     # the filter launch that did the work: the matching kernel with the longest trace time
     # (AUTO's gated re-run launches the split filter, which exits at once)
     cands = [k for k in counters if "k_gemm_filter" in k or "k_gemm_fused" in k]
+    if not cands:  # the direct-form workloads (config L): the direct kernel
+        cands = [k for k in counters if "k_direct" in k]
     cands.sort(key=lambda k: sum(dur.get(k, [0.0])))
     for k in cands[-1:]:
         c = counters[k]

@@ -68,3 +68,44 @@ def test_clustered_fused_vs_direct_and_oracle(knn, oracle, monkeypatch, d, k, nt
     finally:
         auto.close()
         direct.close()
+
+
+def test_nonfinite_train_rows_at_filter_size(knn, oracle):
+    """NaN / inf features in a few train rows at a size where AUTO runs the MFMA filter: such a
+    row's norm fails the certificate's range check (k_row_norms: !(norm < 2^125)), the call
+    takes the exact path, and -- like main.cpp:47's strict '<' -- the rows never become
+    neighbours.  Every query equal to the direct form; a sample equal to the oracle."""
+    import torch
+    dev = "cuda:0"
+    nt, nq, d, k, C = 262_144, 4096, 128, 10, 10
+    auto = knn.Context(0, algo="auto")
+    direct = knn.Context(0, algo="direct")
+    try:
+        train = torch.empty((nt, d), dtype=torch.float32, device=dev)
+        labels = torch.empty(nt, dtype=torch.int32, device=dev)
+        test = torch.empty((nq, d), dtype=torch.float32, device=dev)
+        auto.generate(train, labels, 0, d, 2, 21, 0, C)
+        auto.generate(test, None, 0, d, 2, 21, 1, C)
+        train[5, 3] = float("nan")
+        train[77_777, 0] = float("inf")
+        train[200_000, 127] = float("-inf")
+        out = {}
+        for name, c in (("auto", auto), ("direct", direct)):
+            p = torch.empty(nq, dtype=torch.int32, device=dev)
+            dd = torch.empty((nq, k), dtype=torch.float32, device=dev)
+            ii = torch.empty((nq, k), dtype=torch.int32, device=dev)
+            c.predict_device(train, labels, test, k, C, p, dist=dd, idx=ii)
+            torch.cuda.synchronize()
+            out[name] = (p.cpu().numpy(), dd.cpu().numpy(), ii.cpu().numpy())
+        pa, da, ia = out["auto"]
+        pd, dd_, id_ = out["direct"]
+        assert np.array_equal(ia, id_) and np.array_equal(da.view(np.uint32), dd_.view(np.uint32))
+        assert np.array_equal(pa, pd)
+        assert not np.isin(ia, [5, 77_777, 200_000]).any()
+        qs = np.array([0, 1234, 4095])
+        bad, op, od, oi = oracle.knn(train.cpu().numpy(), labels.cpu().numpy(), test.cpu().numpy()[qs], k, C)
+        assert bad == 0
+        assert np.array_equal(oi, ia[qs]) and np.array_equal(op, pa[qs])
+    finally:
+        auto.close()
+        direct.close()
