@@ -678,9 +678,9 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // Lane-parallel slow path.  Passes are sparse (A: a wave-tile has one in about 8 tiles,
     // usually one query, one value), so instead of visiting the passing positions one
     // wave-wide step at a time, every lane takes ITS OWN passing values, one per round, all
-    // lanes at once: a scan of the lane's 16 values of a passing accumulator (v_cmp + selects
-    // per value) yields the highest passing index below the previous round's, its value and
-    // (first round) how many pass; fn(c, idx, y) then handles every lane's candidate together
+    // lanes at once: one scan of the lane's 16 values of a passing accumulator yields its
+    // passing set (a 16-bit mask) and the value of the lowest passing index; later rounds take
+    // the next set bit; fn(c, idx, y) then handles every lane's candidate together
     // (idx < 0: none).  Rounds = the most passing values of one lane in the accumulator (1
     // unless the threshold is still loose).  Any processing order keeps every true neighbour:
     // a row is kept iff L <= the threshold at its turn, and the threshold is always the k-th
@@ -690,38 +690,84 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         for (int c = 0; c < NACC; c++) {
             if (!((u >> (16 * c)) & 1u)) continue;  // (wave-uniform) no lane passes in c
             const float tfc = tf[c / RG];
-            // round 1: the highest passing index, its value, the lane's passing count
-            // (a scan of the 16 values; scanning the highest passing group of four instead,
-            // found by the group minima, measured 4-8 % slower overall: r03q)
-            // (detecting "some lane passes twice" from the compares' wave masks with scalar ops
-            // instead of the count measured 2.7 % slower on B: r03s)
-            int idx = -1, cnt = 0;
+            // round 1, one scan of the lane's 16 values from r = 15 down to 0: the passing set as
+            // a 16-bit mask m = 2m + (y_r <= tf) (v_addc_co_u32 with the compare's VCC as
+            // carry-in) and the value of the LOWEST passing index (v_cndmask on the same VCC) --
+            // three VALU per value in one asm block (no hazard padding between values), no SGPR
+            // mask pairs held.  The lowest passing index is ffs(m) - 1 and "passes twice" is
+            // m & (m - 1); later rounds take the next lowest set bit.  Same box (r05n) against the
+            // compiler's scan (compare + index, value and count selects: ~4.5 VALU per value):
+            // A filter 19.94 -> 19.55 ms, B 465.3 -> 456.7, C1 1683.6 -> 1643.6.
+            // (Scanning the highest passing group of four, found by the group minima, measured
+            // 4-8 % slower: r03q; the count from the compares' wave masks by scalar ops, 2.7 %
+            // slower on B: r03s.)
+            uint32_t m = 0u;
             float yv = INF;
-#pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const bool p = Y[c][r] <= tfc;
-                idx = p ? r : idx;
-                yv = p ? Y[c][r] : yv;
-                cnt += p ? 1 : 0;
-            }
+            asm volatile("v_cmp_le_f32_e32 vcc, %18, %2\n\t"
+                         "v_cndmask_b32_e32 %1, %1, %18, vcc\n\t"
+                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                         "v_cmp_le_f32_e32 vcc, %17, %2\n\t"
+                         "v_cndmask_b32_e32 %1, %1, %17, vcc\n\t"
+                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                         "v_cmp_le_f32_e32 vcc, %16, %2\n\t"
+                         "v_cndmask_b32_e32 %1, %1, %16, vcc\n\t"
+                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                         "v_cmp_le_f32_e32 vcc, %15, %2\n\t"
+                         "v_cndmask_b32_e32 %1, %1, %15, vcc\n\t"
+                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                         "v_cmp_le_f32_e32 vcc, %14, %2\n\t"
+                         "v_cndmask_b32_e32 %1, %1, %14, vcc\n\t"
+                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                         "v_cmp_le_f32_e32 vcc, %13, %2\n\t"
+                         "v_cndmask_b32_e32 %1, %1, %13, vcc\n\t"
+                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                         "v_cmp_le_f32_e32 vcc, %12, %2\n\t"
+                         "v_cndmask_b32_e32 %1, %1, %12, vcc\n\t"
+                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                         "v_cmp_le_f32_e32 vcc, %11, %2\n\t"
+                         "v_cndmask_b32_e32 %1, %1, %11, vcc\n\t"
+                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                         "v_cmp_le_f32_e32 vcc, %10, %2\n\t"
+                         "v_cndmask_b32_e32 %1, %1, %10, vcc\n\t"
+                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                         "v_cmp_le_f32_e32 vcc, %9, %2\n\t"
+                         "v_cndmask_b32_e32 %1, %1, %9, vcc\n\t"
+                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                         "v_cmp_le_f32_e32 vcc, %8, %2\n\t"
+                         "v_cndmask_b32_e32 %1, %1, %8, vcc\n\t"
+                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                         "v_cmp_le_f32_e32 vcc, %7, %2\n\t"
+                         "v_cndmask_b32_e32 %1, %1, %7, vcc\n\t"
+                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                         "v_cmp_le_f32_e32 vcc, %6, %2\n\t"
+                         "v_cndmask_b32_e32 %1, %1, %6, vcc\n\t"
+                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                         "v_cmp_le_f32_e32 vcc, %5, %2\n\t"
+                         "v_cndmask_b32_e32 %1, %1, %5, vcc\n\t"
+                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                         "v_cmp_le_f32_e32 vcc, %4, %2\n\t"
+                         "v_cndmask_b32_e32 %1, %1, %4, vcc\n\t"
+                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                         "v_cmp_le_f32_e32 vcc, %3, %2\n\t"
+                         "v_cndmask_b32_e32 %1, %1, %3, vcc\n\t"
+                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                         : "+v"(m), "+v"(yv)
+                         : "v"(tfc), "v"(Y[c][0]), "v"(Y[c][1]), "v"(Y[c][2]), "v"(Y[c][3]), "v"(Y[c][4]), "v"(Y[c][5]), "v"(Y[c][6]), "v"(Y[c][7]), "v"(Y[c][8]), "v"(Y[c][9]), "v"(Y[c][10]), "v"(Y[c][11]), "v"(Y[c][12]), "v"(Y[c][13]), "v"(Y[c][14]), "v"(Y[c][15])
+                         : "vcc");
+            auto pick = [](uint32_t mm) __attribute__((always_inline)) { return __ffs((int)mm) - 1; };  // lowest set bit
+            int idx = pick(m);  // -1 when nothing passes
             fn(c, idx, yv);
-            // further rounds (some lane has more passing values): the highest passing index
-            // below the last one taken
-            if (__ballot(cnt > 1)) {
-                int lim = idx;
+            if (__ballot((m & (m - 1u)) != 0u)) {
+                m = idx >= 0 ? m ^ (1u << idx) : 0u;
 #pragma unroll 1
                 for (int round = 1; round < 16; round++) {
-                    idx = -1;
+                    if (!__ballot(m != 0u)) break;
+                    idx = pick(m);
                     yv = INF;
 #pragma unroll
-                    for (int r = 0; r < 16; r++) {
-                        const bool p = Y[c][r] <= tfc && r < lim;
-                        idx = p ? r : idx;
-                        yv = p ? Y[c][r] : yv;
-                    }
-                    if (!__ballot(idx >= 0)) break;
+                    for (int r = 0; r < 16; r++) yv = r == idx ? Y[c][r] : yv;
                     fn(c, idx, yv);
-                    lim = idx;
+                    m = idx >= 0 ? m ^ (1u << idx) : 0u;
                 }
             }
         }
