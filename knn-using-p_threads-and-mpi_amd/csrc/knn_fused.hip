@@ -764,8 +764,43 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                     if (!__ballot(m != 0u)) break;
                     idx = pick(m);
                     yv = INF;
-#pragma unroll
-                    for (int r = 0; r < 16; r++) yv = r == idx ? Y[c][r] : yv;
+                    // the value at idx: compare + select per value in one asm block (the
+                    // compiler's form pads each pair with a hazard s_nop)
+                    asm volatile("v_cmp_eq_u32_e32 vcc, 0, %1\n\t"
+                                 "v_cndmask_b32_e32 %0, %0, %2, vcc\n\t"
+                                 "v_cmp_eq_u32_e32 vcc, 1, %1\n\t"
+                                 "v_cndmask_b32_e32 %0, %0, %3, vcc\n\t"
+                                 "v_cmp_eq_u32_e32 vcc, 2, %1\n\t"
+                                 "v_cndmask_b32_e32 %0, %0, %4, vcc\n\t"
+                                 "v_cmp_eq_u32_e32 vcc, 3, %1\n\t"
+                                 "v_cndmask_b32_e32 %0, %0, %5, vcc\n\t"
+                                 "v_cmp_eq_u32_e32 vcc, 4, %1\n\t"
+                                 "v_cndmask_b32_e32 %0, %0, %6, vcc\n\t"
+                                 "v_cmp_eq_u32_e32 vcc, 5, %1\n\t"
+                                 "v_cndmask_b32_e32 %0, %0, %7, vcc\n\t"
+                                 "v_cmp_eq_u32_e32 vcc, 6, %1\n\t"
+                                 "v_cndmask_b32_e32 %0, %0, %8, vcc\n\t"
+                                 "v_cmp_eq_u32_e32 vcc, 7, %1\n\t"
+                                 "v_cndmask_b32_e32 %0, %0, %9, vcc\n\t"
+                                 "v_cmp_eq_u32_e32 vcc, 8, %1\n\t"
+                                 "v_cndmask_b32_e32 %0, %0, %10, vcc\n\t"
+                                 "v_cmp_eq_u32_e32 vcc, 9, %1\n\t"
+                                 "v_cndmask_b32_e32 %0, %0, %11, vcc\n\t"
+                                 "v_cmp_eq_u32_e32 vcc, 10, %1\n\t"
+                                 "v_cndmask_b32_e32 %0, %0, %12, vcc\n\t"
+                                 "v_cmp_eq_u32_e32 vcc, 11, %1\n\t"
+                                 "v_cndmask_b32_e32 %0, %0, %13, vcc\n\t"
+                                 "v_cmp_eq_u32_e32 vcc, 12, %1\n\t"
+                                 "v_cndmask_b32_e32 %0, %0, %14, vcc\n\t"
+                                 "v_cmp_eq_u32_e32 vcc, 13, %1\n\t"
+                                 "v_cndmask_b32_e32 %0, %0, %15, vcc\n\t"
+                                 "v_cmp_eq_u32_e32 vcc, 14, %1\n\t"
+                                 "v_cndmask_b32_e32 %0, %0, %16, vcc\n\t"
+                                 "v_cmp_eq_u32_e32 vcc, 15, %1\n\t"
+                                 "v_cndmask_b32_e32 %0, %0, %17, vcc\n\t"
+                                 : "+v"(yv)
+                                 : "v"(idx), "v"(Y[c][0]), "v"(Y[c][1]), "v"(Y[c][2]), "v"(Y[c][3]), "v"(Y[c][4]), "v"(Y[c][5]), "v"(Y[c][6]), "v"(Y[c][7]), "v"(Y[c][8]), "v"(Y[c][9]), "v"(Y[c][10]), "v"(Y[c][11]), "v"(Y[c][12]), "v"(Y[c][13]), "v"(Y[c][14]), "v"(Y[c][15])
+                                 : "vcc");
                     fn(c, idx, yv);
                     m = idx >= 0 ? m ^ (1u << idx) : 0u;
                 }
