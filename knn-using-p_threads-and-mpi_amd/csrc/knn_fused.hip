@@ -450,7 +450,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         }
     };
     auto step = [&](floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int buf, bool dma_on, const DmaTile& dd,
-                    const float (&tf)[QG], bool pre) -> uint32_t {
+                    const float (&tf)[QG], bool pre, float (&mn_out)[NACC]) -> uint32_t {
         const unsigned char* tile = tiles + buf * TILE;
         const unsigned char* a0p = tile + j * STRIDE + 16 * h;
         const unsigned char* a1p = tile + ((RG == 2 ? 32 : 0) + j) * STRIDE + 16 * h;
@@ -520,6 +520,8 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         uint32_t u = 0u;
 #pragma unroll
         for (int c = 0; c < NACC; c++) u |= __ballot(mn[c] <= tf[c / RG]) != 0ull ? (0xffffu << (16 * c)) : 0u;
+#pragma unroll
+        for (int c = 0; c < NACC; c++) mn_out[c] = mn[c];
         return u;
     };
 
@@ -685,7 +687,8 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // unless the threshold is still loose).  Any processing order keeps every true neighbour:
     // a row is kept iff L <= the threshold at its turn, and the threshold is always the k-th
     // smallest U of kept rows.
-    auto lane_rounds = [&](floatx16 (&Y)[NACC], const float (&tf)[QG], uint32_t u, auto&& fn) __attribute__((always_inline)) {
+    auto lane_rounds = [&](floatx16 (&Y)[NACC], const float (&tf)[QG], const float (&mnY)[NACC], uint32_t u,
+                           auto&& fn) __attribute__((always_inline)) {
 #pragma unroll
         for (int c = 0; c < NACC; c++) {
             if (!((u >> (16 * c)) & 1u)) continue;  // (wave-uniform) no lane passes in c
@@ -703,59 +706,146 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             // slower on B: r03s.)
             uint32_t m = 0u;
             float yv = INF;
-            asm volatile("v_cmp_le_f32_e32 vcc, %18, %2\n\t"
-                         "v_cndmask_b32_e32 %1, %1, %18, vcc\n\t"
-                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
-                         "v_cmp_le_f32_e32 vcc, %17, %2\n\t"
-                         "v_cndmask_b32_e32 %1, %1, %17, vcc\n\t"
-                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
-                         "v_cmp_le_f32_e32 vcc, %16, %2\n\t"
-                         "v_cndmask_b32_e32 %1, %1, %16, vcc\n\t"
-                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
-                         "v_cmp_le_f32_e32 vcc, %15, %2\n\t"
-                         "v_cndmask_b32_e32 %1, %1, %15, vcc\n\t"
-                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
-                         "v_cmp_le_f32_e32 vcc, %14, %2\n\t"
-                         "v_cndmask_b32_e32 %1, %1, %14, vcc\n\t"
-                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
-                         "v_cmp_le_f32_e32 vcc, %13, %2\n\t"
-                         "v_cndmask_b32_e32 %1, %1, %13, vcc\n\t"
-                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
-                         "v_cmp_le_f32_e32 vcc, %12, %2\n\t"
-                         "v_cndmask_b32_e32 %1, %1, %12, vcc\n\t"
-                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
-                         "v_cmp_le_f32_e32 vcc, %11, %2\n\t"
-                         "v_cndmask_b32_e32 %1, %1, %11, vcc\n\t"
-                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
-                         "v_cmp_le_f32_e32 vcc, %10, %2\n\t"
-                         "v_cndmask_b32_e32 %1, %1, %10, vcc\n\t"
-                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
-                         "v_cmp_le_f32_e32 vcc, %9, %2\n\t"
-                         "v_cndmask_b32_e32 %1, %1, %9, vcc\n\t"
-                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
-                         "v_cmp_le_f32_e32 vcc, %8, %2\n\t"
-                         "v_cndmask_b32_e32 %1, %1, %8, vcc\n\t"
-                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
-                         "v_cmp_le_f32_e32 vcc, %7, %2\n\t"
-                         "v_cndmask_b32_e32 %1, %1, %7, vcc\n\t"
-                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
-                         "v_cmp_le_f32_e32 vcc, %6, %2\n\t"
-                         "v_cndmask_b32_e32 %1, %1, %6, vcc\n\t"
-                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
-                         "v_cmp_le_f32_e32 vcc, %5, %2\n\t"
-                         "v_cndmask_b32_e32 %1, %1, %5, vcc\n\t"
-                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
-                         "v_cmp_le_f32_e32 vcc, %4, %2\n\t"
-                         "v_cndmask_b32_e32 %1, %1, %4, vcc\n\t"
-                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
-                         "v_cmp_le_f32_e32 vcc, %3, %2\n\t"
-                         "v_cndmask_b32_e32 %1, %1, %3, vcc\n\t"
-                         "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
-                         : "+v"(m), "+v"(yv)
-                         : "v"(tfc), "v"(Y[c][0]), "v"(Y[c][1]), "v"(Y[c][2]), "v"(Y[c][3]), "v"(Y[c][4]), "v"(Y[c][5]), "v"(Y[c][6]), "v"(Y[c][7]), "v"(Y[c][8]), "v"(Y[c][9]), "v"(Y[c][10]), "v"(Y[c][11]), "v"(Y[c][12]), "v"(Y[c][13]), "v"(Y[c][14]), "v"(Y[c][15])
-                         : "vcc");
+            int idx;
             auto pick = [](uint32_t mm) __attribute__((always_inline)) { return __ffs((int)mm) - 1; };  // lowest set bit
-            int idx = pick(m);  // -1 when nothing passes
+            if constexpr (KR <= 32) {
+                // k <= 32 (lists of 16): the value is the fast test's minimum -- a lane with ONE
+                // passing value passes with its minimum, so the scan only builds the passing mask
+                // (compare + add-with-carry, 2 VALU per value); only when some lane passes twice, a
+                // second mask of the positions equal to the minimum picks its index.  Same box (r05p):
+                // A filter 20.07 -> 19.85 ms, B 466.7 -> 463.3; C1 (k = 100: more lanes pass twice,
+                // each paying the second mask) 1677 -> 1687, so KR = 104 keeps the value scan
+                asm volatile("v_cmp_le_f32_e32 vcc, %17, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %16, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %15, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %14, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %13, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %12, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %11, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %10, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %9, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %8, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %7, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %6, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %5, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %4, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %3, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %2, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             : "+v"(m)
+                             : "v"(tfc), "v"(Y[c][0]), "v"(Y[c][1]), "v"(Y[c][2]), "v"(Y[c][3]), "v"(Y[c][4]), "v"(Y[c][5]), "v"(Y[c][6]), "v"(Y[c][7]), "v"(Y[c][8]), "v"(Y[c][9]), "v"(Y[c][10]), "v"(Y[c][11]), "v"(Y[c][12]), "v"(Y[c][13]), "v"(Y[c][14]), "v"(Y[c][15])
+                             : "vcc");
+                yv = mnY[c];
+                if (__ballot((m & (m - 1u)) != 0u)) {
+                    uint32_t e = 0u;
+                    asm volatile("v_cmp_eq_f32_e32 vcc, %17, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_eq_f32_e32 vcc, %16, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_eq_f32_e32 vcc, %15, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_eq_f32_e32 vcc, %14, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_eq_f32_e32 vcc, %13, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_eq_f32_e32 vcc, %12, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_eq_f32_e32 vcc, %11, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_eq_f32_e32 vcc, %10, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_eq_f32_e32 vcc, %9, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_eq_f32_e32 vcc, %8, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_eq_f32_e32 vcc, %7, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_eq_f32_e32 vcc, %6, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_eq_f32_e32 vcc, %5, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_eq_f32_e32 vcc, %4, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_eq_f32_e32 vcc, %3, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_eq_f32_e32 vcc, %2, %1\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                                 : "+v"(e)
+                                 : "v"(yv), "v"(Y[c][0]), "v"(Y[c][1]), "v"(Y[c][2]), "v"(Y[c][3]), "v"(Y[c][4]), "v"(Y[c][5]), "v"(Y[c][6]), "v"(Y[c][7]), "v"(Y[c][8]), "v"(Y[c][9]), "v"(Y[c][10]), "v"(Y[c][11]), "v"(Y[c][12]), "v"(Y[c][13]), "v"(Y[c][14]), "v"(Y[c][15])
+                                 : "vcc");
+                    idx = pick(m & e);
+                } else {
+                    idx = pick(m);
+                }
+            } else {
+                asm volatile("v_cmp_le_f32_e32 vcc, %18, %2\n\t"
+                             "v_cndmask_b32_e32 %1, %1, %18, vcc\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %17, %2\n\t"
+                             "v_cndmask_b32_e32 %1, %1, %17, vcc\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %16, %2\n\t"
+                             "v_cndmask_b32_e32 %1, %1, %16, vcc\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %15, %2\n\t"
+                             "v_cndmask_b32_e32 %1, %1, %15, vcc\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %14, %2\n\t"
+                             "v_cndmask_b32_e32 %1, %1, %14, vcc\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %13, %2\n\t"
+                             "v_cndmask_b32_e32 %1, %1, %13, vcc\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %12, %2\n\t"
+                             "v_cndmask_b32_e32 %1, %1, %12, vcc\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %11, %2\n\t"
+                             "v_cndmask_b32_e32 %1, %1, %11, vcc\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %10, %2\n\t"
+                             "v_cndmask_b32_e32 %1, %1, %10, vcc\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %9, %2\n\t"
+                             "v_cndmask_b32_e32 %1, %1, %9, vcc\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %8, %2\n\t"
+                             "v_cndmask_b32_e32 %1, %1, %8, vcc\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %7, %2\n\t"
+                             "v_cndmask_b32_e32 %1, %1, %7, vcc\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %6, %2\n\t"
+                             "v_cndmask_b32_e32 %1, %1, %6, vcc\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %5, %2\n\t"
+                             "v_cndmask_b32_e32 %1, %1, %5, vcc\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %4, %2\n\t"
+                             "v_cndmask_b32_e32 %1, %1, %4, vcc\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             "v_cmp_le_f32_e32 vcc, %3, %2\n\t"
+                             "v_cndmask_b32_e32 %1, %1, %3, vcc\n\t"
+                             "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+                             : "+v"(m), "+v"(yv)
+                             : "v"(tfc), "v"(Y[c][0]), "v"(Y[c][1]), "v"(Y[c][2]), "v"(Y[c][3]), "v"(Y[c][4]), "v"(Y[c][5]), "v"(Y[c][6]), "v"(Y[c][7]), "v"(Y[c][8]), "v"(Y[c][9]), "v"(Y[c][10]), "v"(Y[c][11]), "v"(Y[c][12]), "v"(Y[c][13]), "v"(Y[c][14]), "v"(Y[c][15])
+                             : "vcc");
+                idx = pick(m);  // -1 when nothing passes
+            }
             fn(c, idx, yv);
             if (__ballot((m & (m - 1u)) != 0u)) {
                 m = idx >= 0 ? m ^ (1u << idx) : 0u;
@@ -807,7 +897,8 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             }
         }
     };
-    auto slow_rl = [&](floatx16 (&Y)[NACC], int tp, const float (&tf)[QG], const TQ& tq, uint32_t u) {
+    auto slow_rl = [&](floatx16 (&Y)[NACC], int tp, const float (&tf)[QG], const TQ& tq, const float (&mnY)[NACC],
+                       uint32_t u) {
         if constexpr (RL) {
             const int64_t tbase = tile_row(tp);
             auto visit = [&](int c, int idx, float yv) __attribute__((always_inline)) {
@@ -834,7 +925,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                     }
                 }
             };
-            lane_rounds(Y, tf, u, visit);
+            lane_rounds(Y, tf, mnY, u, visit);
 #pragma unroll
             for (int g = 0; g < QG; g++) make_tfb(g);
         }
@@ -1054,14 +1145,15 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         float tf[QG];
 #pragma unroll
         for (int g = 0; g < QG; g++) tf[g] = it > 0 ? tf_of(g, tm_prev.v[g]) : -INF;
-        const uint32_t uY = step(X, Y, it % NBUF, dma_on, dd, tf, POS != 0);
+        float mnY[NACC];
+        const uint32_t uY = step(X, Y, it % NBUF, dma_on, dd, tf, POS != 0, mnY);
         // PAIR: the pair's next tile is resident since its barrier -- its first fragments are
         // read now, so their latency hides under the slow path below
         if (POS != GRP - 1 && it + 1 < ntiles) prefetch((it + 1) % NBUF);
         const uint64_t t2 = now();
         if (!KNN_STUDY_NO_SLOW) {
             if (uY) {
-                if constexpr (RL) slow_rl(Y, it - 1, tf, tm_prev, uY);
+                if constexpr (RL) slow_rl(Y, it - 1, tf, tm_prev, mnY, uY);
                 else if constexpr (DEFER) record(Y, it - 1, tf[0], tm_prev.v[0], uY);
                 else slow(Y, it - 1, tf[0], tm_prev.v[0], uY);
             }
@@ -1113,7 +1205,14 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
 #pragma unroll
         for (int g = 0; g < QG; g++) tf[g] = tf_of(g, tm_prev.v[g]);
         if constexpr (RL) {
-            slow_rl(accB, last, tf, tm_prev, 0xffffffffu);
+            float mnB[NACC];
+#pragma unroll
+            for (int c = 0; c < NACC; c++) {
+                mnB[c] = INF;
+#pragma unroll
+                for (int v = 0; v < 16; v++) mnB[c] = fminf(mnB[c], accB[c][v]);
+            }
+            slow_rl(accB, last, tf, tm_prev, mnB, 0xffffffffu);
         } else {
             if (pass_set(accB, tf[0], 0xffffffffu)) {
                 if constexpr (DEFER) record(accB, last, tf[0], tm_prev.v[0], 0xffffffffu);
