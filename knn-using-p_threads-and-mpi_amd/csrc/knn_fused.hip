@@ -527,16 +527,19 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
 
     // append candidate (L, U) of global row t to query group g's sub-slice of this lane half
     // (past its capacity: counted only, the rescore then sends the query to the exact scan)
-    auto store_cand = [&](int g, float L, float U, int64_t t) __attribute__((always_inline)) {
+    auto store_cand32 = [&](int g, float L, float U, int32_t t) __attribute__((always_inline)) {
 #ifndef KNN_STUDY_NO_STORE
         if (ccnt[g] < cap_sub) {
             const int64_t o = q[g] * (int64_t)a.cap + (int64_t)(2 * seg + h) * cap_sub + ccnt[g];
-            a.cand[o] = CandRec{(int32_t)t, L, U};
+            a.cand[o] = CandRec{t, L, U};
         }
         ccnt[g]++;
 #else  // (ablation build: no candidate stores, nothing counted -- every query takes the exact scan)
-        asm volatile("" ::"v"(L), "v"(U), "v"((int)t));
+        asm volatile("" ::"v"(L), "v"(U), "v"(t));
 #endif
+    };
+    auto store_cand = [&](int g, float L, float U, int64_t t) __attribute__((always_inline)) {
+        store_cand32(g, L, U, (int32_t)t);
     };
     // (heap shapes, QG = 1) keep candidate (L, U) of global row t: the exact test against the
     // current threshold, the candidate store into this lane half's sub-slice, and, if U beats
@@ -667,10 +670,17 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
 #pragma unroll
             for (int i = 0; i < LL; i++) lst[g][i] = i < pads ? -INF : INF;
     }
+    // min as v_med3 against a -inf the compiler cannot see: with a literal -inf it folds the
+    // med3 back into v_min_f32 and canonicalises both inputs (two more v_max per min)
+    float ninf_op;
+    asm("s_mov_b32 %0, 0xff800000" : "=s"(ninf_op));
+    auto fmin_op = [&](float a, float b) __attribute__((always_inline)) {
+        return __builtin_amdgcn_fmed3f(a, b, ninf_op);
+    };
     auto list_insert = [&](int g, float w) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = LL - 1; i >= 1; i--) lst[g][i] = __builtin_amdgcn_fmed3f(lst[g][i - 1], w, lst[g][i]);
-        lst[g][0] = fmin_fast(lst[g][0], w);
+        lst[g][0] = fmin_op(lst[g][0], w);
     };
     // the other lane half's copy of a word (v_permlane32_swap: one of the swap's two results
     // is this lane's own word, the other its partner's)
@@ -901,6 +911,8 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                        uint32_t u) {
         if constexpr (RL) {
             const int64_t tbase = tile_row(tp);
+            // (the band's half-width hoisted per tile and 32-bit row compares measured no faster:
+            // r05q)
             auto visit = [&](int c, int idx, float yv) __attribute__((always_inline)) {
                 const int g = c / RG;
                 const int row = 32 * (c % RG) + (idx & 3) + 8 * (idx >> 2) + 4 * h;
@@ -913,7 +925,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                 if constexpr (HALVES) {
                     if (__ballot(w < INF)) {
                         list_insert(g, w);
-                        thr[g] = fmin_fast(thr[g], __builtin_amdgcn_fmed3f(lst[g][LL - 1], partner(lst[g][LL - 1]), INF));
+                        thr[g] = fmin_op(thr[g], __builtin_amdgcn_fmed3f(lst[g][LL - 1], partner(lst[g][LL - 1]), INF));
                     }
                 } else {
                     // (no lane inserting means no partner inserting: the swap waits for one)
@@ -921,7 +933,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                         const float wp = partner(w);  // the other half's candidate
                         list_insert(g, w);
                         list_insert(g, wp);
-                        thr[g] = fmin_fast(thr[g], lst[g][LL - 1]);
+                        thr[g] = fmin_op(thr[g], lst[g][LL - 1]);
                     }
                 }
             };

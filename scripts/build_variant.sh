@@ -14,7 +14,7 @@ make -s libknn_amd.so
 mkdir -p build/study
 SRC=csrc/.variant_${NAME}.hip
 if [ "$REV" = "." ]; then cp csrc/knn_fused.hip $SRC; else git show "$REV:knn-using-p_threads-and-mpi_amd/csrc/knn_fused.hip" > $SRC; fi
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" -c -o build/study/knn_fused_$NAME.o $SRC
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -fno-slp-vectorize "$@" -c -o build/study/knn_fused_$NAME.o $SRC
 rm -f $SRC
 KOBJ=build/knn_kernels.o
 if [ "$KERNELS" = 1 ]; then
