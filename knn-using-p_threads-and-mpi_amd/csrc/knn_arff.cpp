@@ -348,6 +348,7 @@ uint64_t knn_flat_view_uid() {
 }
 
 int knn_ctx_device(const knn_ctx* c);  // (knn_capi.cpp: the device a context drives)
+void* knn_ctx_stream(const knn_ctx* c);  // (knn_capi.cpp: its stream)
 
 namespace {
 
@@ -463,14 +464,19 @@ void predict_range_train_sharded(const KnnFlatView& tr, const KnnFlatView& te, i
             DevMem dt(dev, tb), dl(dev, sizeof(int32_t) * (size_t)(t1 - t0)), dq(dev, qb);
             rec[g].reset(new DevMem(dev, recb));
             if (!dt.p || !dl.p || !dq.p || !rec[g]->p) { st[g] = KNN_ENOMEM; why[g] = "device allocation"; return; }
-            if (hipMemcpy(dt.p, tr.feat.data() + (size_t)t0 * tr.ld, tb, hipMemcpyHostToDevice) != hipSuccess ||
-                hipMemcpy(dl.p, tr.labels.data() + t0, sizeof(int32_t) * (size_t)(t1 - t0), hipMemcpyHostToDevice) != hipSuccess ||
-                hipMemcpy(dq.p, te.feat.data() + (size_t)q0 * te.ld, qb, hipMemcpyHostToDevice) != hipSuccess) {
+            // uploads on the context's own stream, so the shard pass is ordered after them (a
+            // null-stream hipMemcpy may return before its DMA lands, and the context's stream
+            // does not wait for the null stream)
+            hipStream_t sg = (hipStream_t)knn_ctx_stream(cs[g]);
+            if (hipMemcpyAsync(dt.p, tr.feat.data() + (size_t)t0 * tr.ld, tb, hipMemcpyHostToDevice, sg) != hipSuccess ||
+                hipMemcpyAsync(dl.p, tr.labels.data() + t0, sizeof(int32_t) * (size_t)(t1 - t0), hipMemcpyHostToDevice,
+                               sg) != hipSuccess ||
+                hipMemcpyAsync(dq.p, te.feat.data() + (size_t)q0 * te.ld, qb, hipMemcpyHostToDevice, sg) != hipSuccess) {
                 st[g] = KNN_EHIP; why[g] = "upload"; return;
             }
             knn_dataset dtr{dt.p, (const int32_t*)dl.p, t1 - t0, tr.d, tr.ld, KNN_F32};
             knn_dataset dte{dq.p, nullptr, nq, te.d, te.ld, KNN_F32};
-            st[g] = knn_shard_topk_device(cs[g], &dtr, &dte, k, C, t0, (int32_t*)rec[g]->p, nullptr);
+            st[g] = knn_shard_topk_device(cs[g], &dtr, &dte, k, C, t0, (int32_t*)rec[g]->p, sg);
             if (st[g] != KNN_OK) why[g] = knn_last_error(cs[g]);
         };
         th.emplace_back(job);
@@ -483,12 +489,16 @@ void predict_range_train_sharded(const KnnFlatView& tr, const KnnFlatView& te, i
     const int dev0 = knn_ctx_device(cs[0]);
     DevMem all(dev0, recb * (size_t)G), pred(dev0, sizeof(int32_t) * (size_t)nq);
     if (!all.p || !pred.p) throwf("KNN (train-sharded): device allocation failed");
-    for (int g = 0; g < G; g++)
-        if (hipMemcpyPeer((char*)all.p + recb * (size_t)g, dev0, rec[g]->p, rec[g]->dev, recb) != hipSuccess)
-            throwf("KNN (train-sharded): copy of shard %d's lists failed", g);
+    // the gather on device 0's context stream, ahead of the merge on the same stream (round 5: a
+    // null-stream hipMemcpyPeer returned before its copy landed and the merge, on the context's
+    // non-blocking stream, read half-copied records -- "a train label is outside [0, C)")
     (void)hipSetDevice(dev0);
+    hipStream_t s0 = (hipStream_t)knn_ctx_stream(cs[0]);
+    for (int g = 0; g < G; g++)
+        if (hipMemcpyPeerAsync((char*)all.p + recb * (size_t)g, dev0, rec[g]->p, rec[g]->dev, recb, s0) != hipSuccess)
+            throwf("KNN (train-sharded): copy of shard %d's lists failed", g);
     const knn_status s = knn_merge_vote_device(cs[0], G, nq, k, C, (const int32_t*)all.p, (int32_t*)pred.p, nullptr,
-                                               nullptr, nullptr);
+                                               nullptr, s0);
     if (s != KNN_OK) throwf("KNN (train-sharded merge): %s (status %d)", knn_last_error(cs[0]), (int)s);
     if (hipMemcpy(out, pred.p, sizeof(int32_t) * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess)
         throwf("KNN (train-sharded): download failed");

@@ -199,7 +199,8 @@ knn_status knn_comm_create(knn_ctx* ctx, const void* id, int32_t nranks, int32_t
         knn_comm_destroy(c);
         return KNN_ENOMEM;
     }
-    if (hipMemcpy(c->flag, words, sizeof(words), hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMemcpy(c->flag, words, sizeof(words), hipMemcpyHostToDevice) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {  // (landed before any stream of the comm reads it)
         knn_comm_destroy(c);
         return KNN_EHIP;
     }
