@@ -259,12 +259,11 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     constexpr bool PAIR = GRP > 1;
     constexpr int AHEAD = PAIR ? GRP : NBUF - 1;  // tiles between a step and the tile it DMAs
     static_assert(RG == 1 || RG == 2, "row groups");
-    static_assert(KR == 0 || KR == 16 || KR == 32 || KR == 104, "register lists: k <= 16, 32, 104, or LDS heaps");
+    static_assert(KR == 0 || KR == 8 || KR == 32 || KR == 104, "register lists: k <= 16, 32, 104, or LDS heaps");
     constexpr bool RL = KR > 0;                   // thresholds from per-lane register lists (else LDS heaps)
     // (QG = 2 on 64-row tiles, four accumulators, was tried at d = 64: 1.5 KB of scratch spills)
     static_assert(QG == 1 || (QG == 2 && RG == 1 && RL), "64-query waves: 32-row tiles, register lists");
-    constexpr bool HALVES = KR >= 32;             // one list per lane half (below): k <= 2 LL
-    constexpr int LL = KR == 104 ? 52 : 16;       // register list length
+    constexpr int LL = KR == 104 ? 52 : KR == 8 ? 8 : 16;  // register list length (one per lane half)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* tiles = smem;                                     // [NBUF][TILE]
     const int hs = heap_stride(a.k);
@@ -649,22 +648,19 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         publish();
     };
 
-    // register-list slow path (KR > 0), k <= 16: both lanes of a query (its two row halves)
-    // keep the same ascending list lst[] of the 16 smallest U of the query's kept candidates
-    // -- the first 16 - k entries are -inf pads, so lst[15] is the k-th smallest real U, an
-    // upper bound on D_(k) (k rows with D <= U <= it).  Per passing value the two lanes swap
-    // their candidate U (v_permlane32_swap) and both insert both (32 v_med3, the multiset and
-    // so the list come out the same in either order): the query's exact k-th smallest, like
-    // the heap, for all 32 queries of the wave at once -- no LDS, no lane takes turns.
-    // HALVES (16 < k <= 32, KR = 32, LL = 16; 32 < k <= 104, KR = 104, LL = 52): each lane
-    // keeps its own half's ceil(k/2) smallest U (LL - ceil(k/2) pads) and inserts only its own
-    // values (LL v_med3); the bound is the larger of the two
-    // halves' ceil(k/2)-th smallest -- at least 2 ceil(k/2) >= k kept rows have U <= it.  A
-    // little looser than the exact k-th smallest, with no LDS heap and no turn-taking.
-    // (QG = 2: one list per query group.)
+    // register-list slow path (KR > 0): the two lanes of a query (its two row halves) each keep
+    // an ascending list lst[] of their own half's ceil(k/2) smallest U (k <= 16: KR = 8, LL = 8;
+    // k <= 32: KR = 32, LL = 16; 32 < k <= 104: KR = 104, LL = 52; the first LL - ceil(k/2)
+    // entries are -inf pads) and insert only their own values (LL v_med3); the bound is the
+    // larger of the two halves' ceil(k/2)-th smallest -- at least 2 ceil(k/2) >= k kept rows
+    // have U <= it.  A little looser than the exact k-th smallest, with no LDS heap and no lane
+    // taking turns, for all queries of the wave at once.  (Until round 5, k <= 16 kept one exact
+    // 16-entry list in both lanes, each inserting both lanes' values: 32 v_med3 and a lane swap
+    // per insert; the halves keep ~20 % more candidates and measured A 20.05 -> 19.84 ms, its
+    // 8-GPU share 3.05 -> 2.97 ms, same box, r05v.)  (QG = 2: one list per query group.)
     float lst[QG][RL ? LL : 1];
     if constexpr (RL) {
-        const int pads = LL - (HALVES ? (k + 1) / 2 : k);
+        const int pads = LL - (k + 1) / 2;
 #pragma unroll
         for (int g = 0; g < QG; g++)
 #pragma unroll
@@ -922,19 +918,9 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                 const bool keep = idx >= 0 && t < row_end && L <= thr[g];
                 if (keep) store_cand(g, L, U, t);
                 const float w = (keep && U < lst[g][LL - 1]) ? U : INF;
-                if constexpr (HALVES) {
-                    if (__ballot(w < INF)) {
-                        list_insert(g, w);
-                        thr[g] = fmin_op(thr[g], __builtin_amdgcn_fmed3f(lst[g][LL - 1], partner(lst[g][LL - 1]), INF));
-                    }
-                } else {
-                    // (no lane inserting means no partner inserting: the swap waits for one)
-                    if (__ballot(w < INF)) {
-                        const float wp = partner(w);  // the other half's candidate
-                        list_insert(g, w);
-                        list_insert(g, wp);
-                        thr[g] = fmin_op(thr[g], lst[g][LL - 1]);
-                    }
+                if (__ballot(w < INF)) {
+                    list_insert(g, w);
+                    thr[g] = fmin_op(thr[g], __builtin_amdgcn_fmed3f(lst[g][LL - 1], partner(lst[g][LL - 1]), INF));
                 }
             };
             lane_rounds(Y, tf, mnY, u, visit);
@@ -1036,7 +1022,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // pieces' rows are disjoint and every published value is the U of a kept row.  Any value
     // read may be stale or from a list being rewritten: a list only ever lowers its entries
     // position by position, so a stale mix counts no more rows below a bound than the current
-    // list holds (a looser bound, never a wrong one).  HALVES: per lane half (its rows), the
+    // list holds (a looser bound, never a wrong one).  Per lane half (its rows), the
     // bound the larger of the two halves' union values.
     auto list_share_now = [&](int it) __attribute__((always_inline)) {
         return (it >= KNN_FUSED_LIST_FIRST && ((it + 1) & it) == 0) || (it & (KNN_FUSED_LIST_EVERY - 1)) == KNN_FUSED_LIST_EVERY - 1;
@@ -1046,8 +1032,8 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             const int W = a.lshare_w;
 #pragma unroll
             for (int g = 0; g < QG; g++) {
-                float* base = a.lshare + ((qvalid[g] ? q[g] : 0) * (int64_t)a.nseg) * W + (HALVES ? 16 * h : 0);
-                if (qvalid[g] && (HALVES || h == 0)) {
+                float* base = a.lshare + ((qvalid[g] ? q[g] : 0) * (int64_t)a.nseg) * W + LL * h;
+                if (qvalid[g]) {
                     uint32_t* dst = reinterpret_cast<uint32_t*>(base + (int64_t)seg * W);
 #pragma unroll
                     for (int i = 0; i < LL; i++)
@@ -1060,7 +1046,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                 // a published list: +inf at the pad positions [0, pads), then its real values
                 // ascending (+inf where not filled yet) -- reading starts at the chunk holding the
                 // first real value, and a chunk whose smallest value no lane can take ends it
-                const int pads = LL - (HALVES ? (k + 1) / 2 : k);
+                const int pads = LL - (k + 1) / 2;
                 for (int p = 0; p < a.nseg; p++) {
                     if (p == seg) continue;
                     const uint32_t* src = reinterpret_cast<const uint32_t*>(base + (int64_t)p * W);
@@ -1083,7 +1069,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                         }
                     }
                 }
-                const float ub = HALVES ? __builtin_amdgcn_fmed3f(tmp[LL - 1], partner(tmp[LL - 1]), INF) : tmp[LL - 1];
+                const float ub = __builtin_amdgcn_fmed3f(tmp[LL - 1], partner(tmp[LL - 1]), INF);
                 if (qvalid[g] && ub < thr[g]) {
                     thr[g] = ub;
                     make_tfb(g);
@@ -1094,7 +1080,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // one tile of the scan; posc: the tile's place in its barrier group (it % GRP), static
     auto iter = [&](auto posc, floatx16 (&X)[NACC], floatx16 (&Y)[NACC], int it) {
         constexpr int POS = decltype(posc)::value;
-        if constexpr (RL && QG == 1 && LL == 16 && KNN_FUSED_LIST_SHARE) {
+        if constexpr (RL && QG == 1 && KR <= 32 && KNN_FUSED_LIST_SHARE) {
             if (a.lshare && list_share_now(it)) exchange_lists();
         }
         if (share_now(it)) {
@@ -1362,8 +1348,8 @@ static size_t fused_lds_of(int row_bytes, int k, int nw, int rg, int nbuf, bool 
 }
 
 int knn_fused_list_share_width(const FilterPlan& f) {
-    if (!KNN_FUSED_LIST_SHARE || !f.ls || !(f.kr == 16 || f.kr == 32)) return 0;
-    return f.kr == 32 ? 32 : 16;
+    if (!KNN_FUSED_LIST_SHARE || !f.ls || !(f.kr == 8 || f.kr == 32)) return 0;
+    return f.kr == 32 ? 32 : 16;  // (two lane halves' lists)
 }
 
 bool knn_fused_supported(int d) { return d == 64 || d == 128 || d == 256; }
@@ -1374,7 +1360,7 @@ bool knn_fused_supported(int d) { return d == 64 || d == 128 || d == 256; }
 int knn_fused_row_bytes(int d) { return d == 64 && KNN_FUSED_AUG64 ? 2 * d + 32 : 2 * d; }
 
 // Shapes (d = features; rows of 2d bytes).  Block = NW waves x 32 QG queries:
-//  * k <= 32 (register lists, KR = 16 / 32): 8 waves; 64 queries per wave on 32-row tiles in
+//  * k <= 32 (register lists, KR = 8 / 32): 8 waves; 64 queries per wave on 32-row tiles in
 //    octets for large query counts (below), else 32 per wave on 64-row tiles -- in quads when
 //    eight buffers fit (d <= 128), else in pairs (four buffers, one barrier per two tiles:
 //    A 33.4 -> 31.3 ms against two buffers, round 2; 8-wave blocks: B 765 -> 743 ms).
@@ -1382,8 +1368,8 @@ int knn_fused_row_bytes(int d) { return d == 64 && KNN_FUSED_AUG64 ? 2 * d + 32 
 //  * k > 32 otherwise (LDS heaps, KR = 0): d = 64 in 4-wave blocks, two buffers, two blocks per
 //    CU (the other block hides the per-tile barrier and fast test of 5-step tiles); d >= 128 in
 //    8-wave blocks: pairs when they fit beside the heaps, else two buffers, else 32-row tiles.
-// Register lists: k <= 16 keeps per-query lists (KR = 16), k <= 32 per-half lists (KR = 32,
-// 16 entries: exact 32-entry lists cost a block per CU of occupancy and 9 % of time on B).
+// Register lists, one per lane half: k <= 16 8 entries (KR = 8), k <= 32 16 (KR = 32: exact
+// 32-entry lists cost a block per CU of occupancy and 9 % of time on B).
 FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus, const FusedForce& force) {
     const int rb = knn_fused_row_bytes(d);
     const size_t cap = 160 * 1024 - 256;  // room for the kernel's static LDS
@@ -1391,7 +1377,7 @@ FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus, const FusedForc
     // the tile buffers get the LDS the heaps held -- 32-row tiles in quads (one barrier per 128
     // rows) instead of one barrier per 32-row tile (force.heaps: the heap shape).  (64-row
     // tiles in pairs, the other way to the same barrier count, spill: two more accumulators.)
-    const int kr = k <= 16 ? 16 : k <= 32 ? 32 : (k <= 104 && d == 256 && !force.heaps) ? 104 : 0;
+    const int kr = k <= 16 ? 8 : k <= 32 ? 32 : (k <= 104 && d == 256 && !force.heaps) ? 104 : 0;
     auto make = [&](int nw, int rg, int minw, int nbuf, int qg = 1) {
         FilterPlan f{nw, qg, rg, minw, nbuf, 32 * qg * nw, fused_lds_of(rb, k, nw, rg, nbuf, kr == 0, qg)};
         f.kr = kr;
@@ -1460,7 +1446,7 @@ template <int RB>
 static const void* fused_fn(const FilterPlan& f) {
     if constexpr (RB == 512)
         if (f.kr == 104) return fused_fn_k<RB, 104>(f);
-    return f.kr == 16 ? fused_fn_k<RB, 16>(f) : f.kr == 32 ? fused_fn_k<RB, 32>(f) : fused_fn_k<RB, 0>(f);
+    return f.kr == 8 ? fused_fn_k<RB, 8>(f) : f.kr == 32 ? fused_fn_k<RB, 32>(f) : fused_fn_k<RB, 0>(f);
 }
 
 static const void* fused_ptr(int d, const FilterPlan& f) {
