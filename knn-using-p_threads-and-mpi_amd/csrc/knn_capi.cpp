@@ -274,11 +274,11 @@ int choose_direct_segments(const knn_ctx* c, int64_t nt, int64_t nq, int d, int 
     const int64_t nqb = (nq + qb - 1) / qb;
     const int64_t slots = (int64_t)occ * c->num_cus;
     if (qb < knn_direct_tile_qb(k)) {
-        // k_direct_rows (a wave per unit): enough units for half the resident waves -- its
-        // waves need no co-residents to hide a barrier, and every segment adds a sorted first
-        // tile and a merge source (config L, 430 query groups: 4 segments 0.101 ms, 8 0.097,
-        // 16 (a full round) 0.104, 32 0.131; r05c)
-        const int64_t want = (slots / 2 + nqb - 1) / nqb;
+        // k_direct_rows (a wave per unit): about one round of resident waves -- its waves need
+        // no co-residents to hide a barrier, and every segment adds a sorted first tile and a
+        // merge source (config L, 859 query pairs, same box: 4 segments 0.092 ms, 5 0.094, 8
+        // 0.089, 12 0.097, 16 0.103, 32 0.131; r05y)
+        const int64_t want = (slots + nqb / 2) / nqb;
         int64_t s = std::max<int64_t>(1, std::min<int64_t>(want, 32));
         while (s > 1 && nt / s < 256) s--;
         while (s > 1 && (double)s * (double)nq * 12.0 * k > 2e9) s--;

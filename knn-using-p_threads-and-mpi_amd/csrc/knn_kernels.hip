@@ -2134,7 +2134,13 @@ static const void* direct_tile_ptr(int k, int elem) {
 
 // k_direct_rows (d <= 16, k <= 16): DR_QW queries per wave (their features stay in scalar
 // registers), a wave per work unit
-static constexpr int DR_QW = 4;
+// (one query pair per wave: more waves, each with fewer inserts in flight; config L, same box,
+// direct + merge stages: 4 queries per wave 0.097 ms at its best segment count, 2 queries 0.089,
+// 8 queries 0.136 -- r05y)
+#ifndef KNN_DR_QW
+#define KNN_DR_QW 2  // (a study build may set 4 or 8)
+#endif
+static constexpr int DR_QW = KNN_DR_QW;
 static bool direct_rows(int k, int d) { return d <= 16 && k <= 16; }
 template <typename E>
 static const void* direct_rows_fn(int d) {
