@@ -6,14 +6,14 @@ One process per GPU (torchrun for N > 1).  Workload A (default, BASELINE configs
 1,000,000 train x 100,000 query rows x 128-d fp32, k = 10, 10 classes, synthetic rows from
 the counter-based generator generated directly in HBM.  The path partitions by
 query (north_star: test-sharded, train replicated, no data-path collective; the reference's
-MPI_Gatherv of predictions, mpi.cpp:186, is not part of the timed region), so on N GPUs every
-rank owns 100,000 queries of its own (global rows [r*100k, (r+1)*100k)) against the same train
-set: weak scaling, "scaling": "weak" (the contract for a partitioned path).  --strong splits
-the fixed 100k-query set by the reference's rule instead (rank r owns shard_range(100k, N, r),
-multi-thread.cpp:154-158 / mpi.cpp:141-170): the reference's own fixed-problem speed-up.  A
-"step" is one KNN(train, test, k) pass over the resident inputs: norms -> MFMA filter ->
-exact rescore/vote -> fallback.  B (configs[3]) is the same split of 1M queries over a 4M-row
-train set.
+MPI_Gatherv of predictions, mpi.cpp:186, is not part of the timed region), so on N GPUs the
+fixed 100k-query set BASELINE names is split by the reference's rule (rank r owns
+shard_range(100k, N, r), multi-thread.cpp:154-158 / mpi.cpp:141-170): strong scaling, the
+reference's own fixed-problem speed-up, "scaling": "strong".  --weak (a study option, never the
+driver's line) gives every rank 100,000 queries of its own instead (global rows [r*100k,
+(r+1)*100k)).  A "step" is one KNN(train, test, k) pass over the resident inputs: norms -> MFMA
+filter -> exact rescore/vote -> fallback.  B (configs[3]) is the same split of its fixed 1M
+queries over a 4M-row train set.
 
 Config C (BASELINE configs[4]) is train-sharded: 32M bf16 train rows x 1M queries x
 256-d, k = 100; rank r owns train rows shard_range(32M, N, r) and every query, computes
@@ -47,9 +47,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 CONFIGS = {
-    # name: (n_train, n_query (per GPU when weak), d, k, classes, seed, scaling, dtype, sharding)
-    "A": (1_000_000, 100_000, 128, 10, 10, 1, "weak", "f32", "test"),
-    "B": (4_000_000, 1_000_000, 64, 32, 10, 2, "weak", "f32", "test"),
+    # name: (n_train, n_query (total; per GPU under --weak), d, k, classes, seed, scaling, dtype, sharding)
+    "A": (1_000_000, 100_000, 128, 10, 10, 1, "strong", "f32", "test"),
+    "B": (4_000_000, 1_000_000, 64, 32, 10, 2, "strong", "f32", "test"),
     "C": (32_000_000, 1_000_000, 256, 100, 10, 3, "strong", "bf16", "train"),
     "C1": (4_000_000, 1_000_000, 256, 100, 10, 3, "strong", "bf16", "train"),
     "L": (30_803, 1_718, 11, 5, 10, 0, "strong", "f32", "arff"),
@@ -346,6 +346,28 @@ def pmc_traffic(key):
 
 
 XCHECK_LIMIT_S = 180  # the exchange check's watchdog (a hung collective ends the run, line printed)
+XCHECK_TIMEOUT_EXIT = 3  # exit status of a run whose exchange check hung (the line is still printed)
+
+
+def run_with_watchdog(fn, limit_s, line, rank, exit_fn=os._exit):
+    """fn() under a watchdog: if it has not returned after limit_s seconds (a hung RCCL
+    collective cannot be interrupted), rank 0's line is printed with the check's status
+    "timeout" and the process ends with XCHECK_TIMEOUT_EXIT -- a failure torchrun and the driver
+    see, not a success with the hang hidden inside the JSON."""
+    def expired():
+        if line is not None:
+            line["rccl_exchange_check"] = {"status": "timeout", "limit_s": limit_s}
+            print(json.dumps(line), flush=True)
+        print(f"[bench rank {rank}] exchange check timed out", file=sys.stderr, flush=True)
+        sys.stderr.flush()
+        exit_fn(XCHECK_TIMEOUT_EXIT)
+    wd = threading.Timer(limit_s, expired)
+    wd.daemon = True
+    wd.start()
+    try:
+        return fn()
+    finally:
+        wd.cancel()
 
 
 def rccl_exchange_check(knn, torch, dist, local, world, rank, share, seed):
@@ -414,6 +436,16 @@ def rccl_exchange_check(knn, torch, dist, local, world, rank, share, seed):
     return out
 
 
+def resolve_scaling(sharding, strong=False, weak=False):
+    """The line's scaling.  Default: strong -- BASELINE's fixed problem (A's 100k / B's 1M
+    queries; C's 32M train rows) split over the ranks by the reference's rule, so a --gpus N
+    value is that one problem's throughput (mpi.cpp:141-186).  --weak (test-sharded configs
+    only, a study option) gives every rank a full query set of its own."""
+    if strong and weak:
+        raise SystemExit("--strong and --weak exclude each other")
+    return "weak" if (sharding == "test" and weak) else "strong"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -424,9 +456,11 @@ def main():
     ap.add_argument("--config", default="A", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--strong", action="store_true",
-                    help="test-sharded configs: split the fixed n_query set by the reference's rule "
-                         "(strong scaling) instead of giving every rank n_query rows of its own")
-    ap.add_argument("--weak", action="store_true", help="(the default for test-sharded configs)")
+                    help="(the default) test-sharded configs: split BASELINE's fixed n_query set by the "
+                         "reference's rule (shard_range)")
+    ap.add_argument("--weak", action="store_true",
+                    help="study option, test-sharded configs: every rank gets n_query rows of its own "
+                         "(weak scaling) instead of a share of the fixed set")
     ap.add_argument("--exchange", default="rccl", choices=["rccl", "torch"],
                     help="train-sharded configs: C-ABI RCCL communicator or torch.distributed all-to-all")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-buffer calls")
@@ -490,10 +524,7 @@ def main():
                                     torch.cuda.get_device_properties(local).total_memory)
     elif args.shard:
         sharding = args.shard
-    if sharding == "test":
-        scaling = "strong" if args.strong else "weak"
-    else:
-        scaling = "strong"
+    scaling = resolve_scaling(sharding, args.strong, args.weak)
     kind = 1 if dtype == "bf16" else 0                  # bf16-exact generator values for bf16
     if args.data == "clustered":
         kind += 2                                       # the clustered variants (kinds 2 / 3)
@@ -735,17 +766,8 @@ def main():
     # multi-rank lines: the train-sharded C-ABI path over a real RCCL communicator of all ranks,
     # checked against the whole-train path (KNN_BENCH_XCHECK=1 runs it at one rank too)
     if (world > 1 and not share) or os.environ.get("KNN_BENCH_XCHECK") == "1":
-        def expired():
-            if line is not None:
-                line["rccl_exchange_check"] = {"status": "timeout", "limit_s": XCHECK_LIMIT_S}
-                print(json.dumps(line), flush=True)
-            print(f"[bench rank {rank}] exchange check timed out", file=sys.stderr, flush=True)
-            os._exit(0)
-        wd = threading.Timer(XCHECK_LIMIT_S, expired)
-        wd.daemon = True
-        wd.start()
-        xc = rccl_exchange_check(knn, torch, dist, local, world, rank, share, seed)
-        wd.cancel()
+        xc = run_with_watchdog(lambda: rccl_exchange_check(knn, torch, dist, local, world, rank, share, seed),
+                               XCHECK_LIMIT_S, line, rank)
         if line is not None:
             line["rccl_exchange_check"] = xc
     if line is not None:

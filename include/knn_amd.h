@@ -232,6 +232,13 @@ knn_status knn_comm_count(const knn_comm* comm, int32_t* nranks);
  * a caller that sees KNN_ERCCL can tell "a peer's shard failed, the communicator is fine" (0)
  * from "tear down every rank and build a new communicator" (1). */
 knn_status knn_comm_broken(const knn_comm* comm, int32_t* broken);
+/* The exchange's message plan (round 6).  Every RCCL send / recv of knn_predict_train_sharded
+ * carries at most chunk_elems int32 (<= 0: the default, 64 Mi elements = 256 MiB); with
+ * self_via_rccl = 0 (the default) the rank's own block is a device copy, with 1 it goes through
+ * the same grouped ncclSend / ncclRecv loop as the peers' blocks -- so a one-rank communicator
+ * executes the multi-rank loop's chunk offsets and counts (the GPU test of that loop; a one-GPU
+ * box cannot hold two RCCL ranks).  Not collective; call it alike on every rank. */
+knn_status knn_comm_set_exchange(knn_comm* comm, int64_t chunk_elems, int32_t self_via_rccl);
 knn_status knn_predict_train_sharded(knn_ctx* ctx, knn_comm* comm, const knn_dataset* train_shard, int64_t idx_base,
                                      const knn_dataset* test, int32_t k, int32_t num_classes, int32_t* d_pred,
                                      float* d_dist, int32_t* d_idx, void* hip_stream);

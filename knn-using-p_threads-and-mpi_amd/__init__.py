@@ -113,6 +113,7 @@ def load_library(path=LIB_PATH):
         "knn_comm_destroy": (None, [P]),
         "knn_comm_count": (I32, [P, ctypes.POINTER(I32)]),
         "knn_comm_broken": (I32, [P, ctypes.POINTER(I32)]),
+        "knn_comm_set_exchange": (I32, [P, I64, I32]),
         "knn_predict_train_sharded": (I32, [P, P, DS, I64, DS, I32, I32, P, P, P, P]),
         "knn_shard_range": (I32, [I64, I32, I32, ctypes.POINTER(I64), ctypes.POINTER(I64)]),
         "knn_shard_policy": (I32, [I64, I64, I32, I32, I32, I64, ctypes.POINTER(I32)]),
@@ -599,6 +600,14 @@ class Comm:
         if st != KNN_OK:
             raise KnnError(st, "knn_comm_count")
         return n.value
+
+    def set_exchange(self, chunk_elems=0, self_via_rccl=False):
+        """knn_comm_set_exchange: RCCL messages of at most chunk_elems int32 (0: the default,
+        256 MiB); self_via_rccl sends the rank's own block through the RCCL loop too (a one-rank
+        communicator then runs the multi-rank exchange's offsets and counts)."""
+        st = self.lib.knn_comm_set_exchange(self.h, int(chunk_elems), 1 if self_via_rccl else 0)
+        if st != KNN_OK:
+            raise KnnError(st, "knn_comm_set_exchange")
 
     def broken(self):
         """True once a collective failed and the communicator was aborted (knn_comm_broken)."""

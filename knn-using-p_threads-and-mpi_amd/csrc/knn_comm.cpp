@@ -91,6 +91,12 @@ bool rccl_ok() {
 
 }  // namespace
 
+// int32 elements per RCCL send / recv of the exchange (knn_comm_set_exchange overrides it per
+// communicator): 64 Mi = 256 MiB
+#ifndef KNN_XCHG_CHUNK
+#define KNN_XCHG_CHUNK ((int64_t)64 << 20)
+#endif
+
 struct knn_comm {
     ncclComm_t comm = nullptr;
     int32_t nranks = 0, rank = 0, device = 0;
@@ -106,6 +112,10 @@ struct knn_comm {
     int32_t* flag = nullptr;
     int32_t* flag_host = nullptr;  // pinned copy of the vote's result
     bool broken = false;           // aborted after a failed collective: every later call fails
+    // the exchange's message plan (knn_comm_set_exchange): int32 elements per RCCL message, and
+    // whether the own block takes the RCCL loop too (else a device copy)
+    int64_t chunk = KNN_XCHG_CHUNK;
+    bool self_rccl = false;
     std::string err;
 };
 
@@ -229,6 +239,13 @@ knn_status knn_comm_broken(const knn_comm* c, int32_t* broken) {
     return KNN_OK;
 }
 
+knn_status knn_comm_set_exchange(knn_comm* c, int64_t chunk_elems, int32_t self_via_rccl) {
+    if (!c || (self_via_rccl != 0 && self_via_rccl != 1)) return KNN_EINVAL;
+    c->chunk = chunk_elems > 0 ? chunk_elems : KNN_XCHG_CHUNK;
+    c->self_rccl = self_via_rccl == 1;
+    return KNN_OK;
+}
+
 void knn_comm_destroy(knn_comm* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
@@ -296,25 +313,28 @@ knn_status knn_predict_train_sharded(knn_ctx* ctx, knn_comm* comm, const knn_dat
     int64_t so[1024], sc[1024], ro[1024], rc[1024];
     knn_exchange_layout(nq, k, comm->nranks, comm->rank, so, sc, ro, rc);
     knn_ctx_stage_begin(ctx, st, "exchange");
-    // this rank's own block is a device copy; the peers' blocks go through RCCL in pieces of at
-    // most KNN_XCHG_CHUNK elements.  (Round 5: a one-rank communicator's grouped self send/recv of
-    // config C1's 1.2 GB of records delivered only its first half -- the queries past ~500k got
-    // wrong neighbour lists, r05i -- so no transfer relies on a single multi-GB RCCL message.)
-    constexpr size_t KNN_XCHG_CHUNK = (size_t)64 << 20;  // 256 MiB of int32 per send / recv
-    if (sc[comm->rank] > 0 &&
+    // this rank's own block is a device copy (unless comm->self_rccl); the other blocks go
+    // through one group of RCCL sends / receives, each of at most comm->chunk elements.
+    // (Round 5: a one-rank communicator's grouped self send/recv of config C1's 1.2 GB of records
+    // delivered only its first half -- the queries past ~500k got wrong neighbour lists, r05i --
+    // so no transfer relies on a single multi-GB RCCL message; DESIGN.md "Multi-GPU" has what
+    // round 6 measured of that failure.)
+    const int64_t chunk = comm->chunk;
+    const bool self_copy = !comm->self_rccl;
+    if (self_copy && sc[comm->rank] > 0 &&
         hipMemcpyAsync((int32_t*)comm->lists + ro[comm->rank], (const int32_t*)comm->rec + so[comm->rank],
                        sizeof(int32_t) * (size_t)sc[comm->rank], hipMemcpyDeviceToDevice, st) != hipSuccess)
         return give_up();  // (every rank takes this branch alike; a failure here is local -- see give_up)
-    if (comm->nranks > 1) {
+    if (comm->nranks > 1 || !self_copy) {
         if (r.group_start() != ncclSuccess) return give_up();
         bool ok = true;
         for (int32_t b = 0; b < comm->nranks && ok; b++) {
-            if (b == comm->rank) continue;
-            for (int64_t o = 0; ok && o < sc[b]; o += (int64_t)KNN_XCHG_CHUNK)
-                ok = r.send((const int32_t*)comm->rec + so[b] + o, (size_t)std::min<int64_t>(KNN_XCHG_CHUNK, sc[b] - o),
+            if (b == comm->rank && self_copy) continue;
+            for (int64_t o = 0; ok && o < sc[b]; o += chunk)
+                ok = r.send((const int32_t*)comm->rec + so[b] + o, (size_t)std::min<int64_t>(chunk, sc[b] - o),
                             ncclInt32, b, comm->comm, st) == ncclSuccess;
-            for (int64_t o = 0; ok && o < rc[b]; o += (int64_t)KNN_XCHG_CHUNK)
-                ok = r.recv((int32_t*)comm->lists + ro[b] + o, (size_t)std::min<int64_t>(KNN_XCHG_CHUNK, rc[b] - o),
+            for (int64_t o = 0; ok && o < rc[b]; o += chunk)
+                ok = r.recv((int32_t*)comm->lists + ro[b] + o, (size_t)std::min<int64_t>(chunk, rc[b] - o),
                             ncclInt32, b, comm->comm, st) == ncclSuccess;
         }
         if (r.group_end() != ncclSuccess || !ok) return give_up();

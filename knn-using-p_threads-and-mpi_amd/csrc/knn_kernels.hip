@@ -621,7 +621,17 @@ __global__ __launch_bounds__(256) void k_direct_rows(DirectTileArgs a) {
 #pragma unroll
         for (int i = 0; i < QW; i++) {
             const float di = (i & 1) ? acc[i >> 1].y : acc[i >> 1].x;
-            u64 m = __ballot(valid && di < thr[i]);
+            const bool pass = valid && di < thr[i];
+            u64 m = __ballot(pass);
+            if (__popcll(m) > DT_SHIFT_MAX) {
+                // many passing rows (train rows in decreasing distance order, e.g. sorted or
+                // clustered data): one bitonic merge of the tile instead of up to 64 serial lane
+                // shifts -- k_direct_tile's SH guard.  Same result: the merge keeps the
+                // k smallest (distance, index) keys, the shifts insert in row order
+                topk_merge<1>(T[i], pass ? make_key(di, (uint32_t)row) : KEY_NONE);
+                thr[i] = kth_dist(T[i][0], k);
+                m = 0;
+            }
             while (m) {
                 const int b = __builtin_ctzll(m);
                 m &= m - 1;

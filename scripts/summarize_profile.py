@@ -4,7 +4,9 @@
 
 Writes profiles/TAG_kernel_stats.csv (the --stats summary as produced),
 profiles/TAG_pmc_traffic.json (per-launch HBM bytes of k_gemm_filter with the gfx950
-FETCH_SIZE x2 correction, MFMA busy fraction, effective clock) and TAG_pmc_counters.csv.
+FETCH_SIZE x2 correction, MFMA busy fraction, effective clock); the per-dispatch counter dump
+TAG_pmc_counters.csv stays beside the raw outputs (gpurun_out/, scratch: only the summaries are
+evidence).
 Rules (MI355X_MICROARCH.md, HBM section): FETCH_SIZE/WRITE_SIZE are in KiB;
 FETCH_SIZE reads 1/2 of the bytes of a wide coalesced stream on gfx950 -> double it;
 WRITE_SIZE is exact for 16-B streaming stores.  Effective clock = GRBM_GUI_ACTIVE / 8 / wall.
@@ -46,7 +48,7 @@ def main():
                 counters[k][r["Counter_Name"]].append((v, wall))
                 rows_out.append({"pass": p, "kernel": k, "counter": r["Counter_Name"], "value": v,
                                  "wall_s": wall})
-    with open(os.path.join(prof, f"{tag}_pmc_counters.csv"), "w", newline="") as f:
+    with open(os.path.join(src, f"{tag}_pmc_counters.csv"), "w", newline="") as f:
         w = csv.DictWriter(f, fieldnames=["pass", "kernel", "counter", "value", "wall_s"])
         w.writeheader()
         w.writerows(rows_out)

@@ -218,7 +218,13 @@ def test_train_sharded_c_abi_large_exchange(knn):
     """knn_predict_train_sharded with records past 2^30 bytes (700k queries x k = 100: 840 MB):
     round 5 found a one-rank communicator's single RCCL self send/recv of config C1's 1.2 GB
     delivering only its first half (queries past ~500k wrong).  The C-ABI path must equal the
-    shard top-k + merge path on every query: predictions, neighbour indices and distance bits."""
+    shard top-k + merge path on every query -- predictions, neighbour indices and distance bits --
+    under each exchange plan (knn_comm_set_exchange):
+      * the default (own block by device copy, peers in 256 MiB messages);
+      * the own block through the RCCL loop in 1 Mi-element (4 MiB) messages: 201 sends and 201
+        receives in one group, so the multi-rank loop's chunk offsets and counts run on one GPU
+        (VERDICT r5: that loop had never executed);
+      * the own block through the RCCL loop in the default 256 MiB messages (4 per direction)."""
     import torch
     nt, nq, d, k = 20_000, 700_000, 64, 100
     dev = "cuda:0"
@@ -228,22 +234,27 @@ def test_train_sharded_c_abi_large_exchange(knn):
     test = torch.empty((nq, d), dtype=torch.bfloat16, device=dev)
     ctx.generate(train, labels, 0, d, 1, 37, 0, 10)
     ctx.generate(test, None, 0, d, 1, 37, 1, 10)
+    rec = torch.empty((nq, 3, k), dtype=torch.int32, device=dev)
+    ctx.shard_topk_device(train, labels, test, k, 10, 0, rec)
+    pred2 = torch.empty(nq, dtype=torch.int32, device=dev)
+    dist2 = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    idx2 = torch.empty((nq, k), dtype=torch.int32, device=dev)
+    ctx.merge_vote_device(rec.view(1, nq, 3, k), k, 10, pred2, dist2, idx2)
+    del rec
     comm = knn.Comm(ctx, knn.comm_unique_id(), 1, 0)
     try:
-        pred = torch.empty(nq, dtype=torch.int32, device=dev)
-        dist = torch.empty((nq, k), dtype=torch.float32, device=dev)
-        idx = torch.empty((nq, k), dtype=torch.int32, device=dev)
-        comm.predict_train_sharded(train, labels, 0, test, k, 10, pred, dist, idx)
-        rec = torch.empty((nq, 3, k), dtype=torch.int32, device=dev)
-        ctx.shard_topk_device(train, labels, test, k, 10, 0, rec)
-        pred2 = torch.empty(nq, dtype=torch.int32, device=dev)
-        dist2 = torch.empty((nq, k), dtype=torch.float32, device=dev)
-        idx2 = torch.empty((nq, k), dtype=torch.int32, device=dev)
-        ctx.merge_vote_device(rec.view(1, nq, 3, k), k, 10, pred2, dist2, idx2)
-        torch.cuda.synchronize()
-        assert torch.equal(idx, idx2)
-        assert torch.equal(dist.view(torch.int32), dist2.view(torch.int32))
-        assert torch.equal(pred, pred2)
+        for chunk, self_rccl in ((0, False), (1 << 20, True), (0, True)):
+            comm.set_exchange(chunk, self_rccl)
+            pred = torch.full((nq,), -7, dtype=torch.int32, device=dev)
+            dist = torch.full((nq, k), -7.0, dtype=torch.float32, device=dev)
+            idx = torch.full((nq, k), -7, dtype=torch.int32, device=dev)
+            comm.predict_train_sharded(train, labels, 0, test, k, 10, pred, dist, idx)
+            torch.cuda.synchronize()
+            plan = f"chunk={chunk} self_via_rccl={self_rccl}"
+            assert torch.equal(idx, idx2), plan
+            assert torch.equal(dist.view(torch.int32), dist2.view(torch.int32)), plan
+            assert torch.equal(pred, pred2), plan
+        assert comm.lib.knn_comm_set_exchange(comm.h, 0, 2) == knn.KNN_EINVAL
     finally:
         comm.close()
         ctx.close()

@@ -203,3 +203,25 @@ def test_direct_rows_segments_ties_bf16(knn, oracle, splits):
         _check(ctx, oracle, knn.to_bf16_bits(btr), bl, knn.to_bf16_bits(bte), 10, 10, feats=(btr, bte))
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("splits", [0, 1, 5])
+def test_direct_rows_descending_distance(knn, oracle, splits):
+    """Train rows in DEcreasing distance from every query (rows scaled toward the queries'
+    centre): every row of every tile passes the running k-th distance, so each tile takes
+    k_direct_rows' many-pass guard (one bitonic merge instead of up to 64 serial lane shifts,
+    ADVICE r5).  Bit-exact against the oracle; duplicates keep the lower index."""
+    rng = np.random.default_rng(77 + splits)
+    nt, nq, d = 9000, 40, 11
+    v = rng.standard_normal((nt, d)).astype(np.float32)
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    tr = (v * np.linspace(50.0, 1.0, nt, dtype=np.float32)[:, None]).astype(np.float32)
+    tr[6000:6500] = tr[5500:6000]  # equal distances at different indices
+    te = (rng.standard_normal((nq, d)) * 0.01).astype(np.float32)
+    tl = rng.integers(0, 10, size=nt).astype(np.int32)
+    ctx = knn.Context(0, algo="direct", train_splits=splits)
+    try:
+        for k in (1, 5, 16):
+            _check(ctx, oracle, tr, tl, te, k, 10)
+    finally:
+        ctx.close()
