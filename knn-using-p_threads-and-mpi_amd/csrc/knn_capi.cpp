@@ -109,9 +109,10 @@ struct knn_ctx {
     bool stage_open = false;  // the last stage_begin recorded an event (profile = 3 skips some)
     std::vector<float> stage_ms;
     std::vector<const char*> stage_names;
-    int64_t stats[9] = {0, 0, 0, -1, 0, 0, 0, 0, 0};  // candidates, fallback queries, segments, filter
+    int64_t stats[10] = {0, 0, 0, -1, 0, 0, 0, 0, 0, 0};  // candidates, fallback queries, segments, filter
                                                       // operand type, rerun, fused, train / query H2D
                                                       // bytes, train-side filter operands from the cache
+    int subs = 2;                           // candidate sub-slices per segment of the last GEMM pass
     int64_t rerun_stats[3] = {0, -1, 0};    // segments, operand type, fused of AUTO's gated split re-run
     int num_cus = 256;
 };
@@ -460,7 +461,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     HIP_OR_FAIL(c, c->tnp.ensure(sizeof(float) * (nt + 64)));
     HIP_OR_FAIL(c, c->qnorm.ensure(sizeof(float) * nq));
     HIP_OR_FAIL(c, c->gthr.ensure(sizeof(uint32_t) * nq));
-    HIP_OR_FAIL(c, c->cnt.ensure(sizeof(int32_t) * nq * 16));  // [2 * nseg][nq], nseg <= 8
+    HIP_OR_FAIL(c, c->cnt.ensure(sizeof(int32_t) * nq * 32));  // [subs * nseg][nq], subs <= 4, nseg <= 8
     HIP_OR_FAIL(c, c->cand.ensure(sizeof(CandRec) * nq * cap));
     HIP_OR_FAIL(c, c->fb_list.ensure(sizeof(int32_t) * nq));
 
@@ -658,8 +659,10 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     }
     g.status = c->ctrl.as<int32_t>();
     g.gate = gate;
-    if (fused && g.g2 >= 0 && nseg > 1)  // whole query tiles write only sub-slice 0
-        HIP_OR_FAIL(c, hipMemsetAsync(c->cnt.p, 0, sizeof(int32_t) * 2 * nseg * nq, st));
+    // candidate sub-slices per segment: per lane half (32x32 filters), per quarter (k_gemm_fused16)
+    const int subs = fused ? knn_fused_subslices(plan) : 2;
+    if (fused && g.g2 >= 0 && nseg > 1)  // whole query tiles write only their piece's sub-slices
+        HIP_OR_FAIL(c, hipMemsetAsync(c->cnt.p, 0, sizeof(int32_t) * subs * nseg * nq, st));
     stage_begin(c, st, gate ? "gemm_filter_rerun" : "gemm_filter");
     if (fused) HIP_OR_FAIL(c, knn_launch_fused(g, plan, st));
     else HIP_OR_FAIL(c, knn_launch_gemm_filter(g, kelem, rb, st));
@@ -669,7 +672,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     r.train = tr->feat; r.labels = tr->labels; r.ld_t = tr->ld;
     r.test = te->feat; r.ld_q = te->ld; r.nq = nq; r.d = d; r.k = k; r.C = C; r.elem = dtype;
     r.cnt = g.cnt; r.cand = g.cand; r.cap = cap;
-    r.nseg = 2 * nseg; r.cap_seg = g.cap_seg / 2;  // sub-slices: (segment, lane half)
+    r.nseg = subs * nseg; r.cap_seg = g.cap_seg / subs;  // sub-slices: (segment, lane half or quarter)
     r.out = out; r.status = c->ctrl.as<int32_t>();
     r.fb_list = c->fb_list.as<int32_t>(); r.fb_count = c->ctrl.as<int32_t>() + 1;
     r.gate = gate;
@@ -692,6 +695,8 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         c->stats[2] = nseg;
         c->stats[3] = felem;
         c->stats[5] = fused;
+        c->stats[9] = fused ? (plan.m16 ? 16 : 32) : 0;
+        c->subs = subs;
     } else {
         c->rerun_stats[0] = nseg;
         c->rerun_stats[1] = felem;
@@ -726,6 +731,7 @@ knn_status knn_create(knn_ctx** out, const knn_opts* opts) {
     if (const char* e = getenv("KNN_FUSED_QG")) c->fforce.qg = atoi(e);
     if (const char* e = getenv("KNN_FUSED_NBUF")) c->fforce.nbuf = atoi(e);
     c->fforce.heaps = getenv("KNN_FUSED_HEAPS") != nullptr;
+    c->fforce.m16 = getenv("KNN_FUSED_MFMA16") != nullptr && std::atoi(getenv("KNN_FUSED_MFMA16")) == 1;
     c->no_lshare = getenv("KNN_NO_LIST_SHARE") != nullptr;
     c->no_cursor = getenv("KNN_NO_SCAN_CURSOR") != nullptr;
     c->rescore_all = getenv("KNN_RESCORE_ALL") != nullptr;
@@ -895,7 +901,7 @@ knn_dataset offset_rows(const knn_dataset& x, int64_t r0, int64_t n) {
 
 void reset_stats(knn_ctx* c) {
     c->stages.clear();
-    for (int i = 0; i < 9; i++) c->stats[i] = 0;
+    for (int i = 0; i < 10; i++) c->stats[i] = 0;
     c->stats[3] = -1;
 }
 
@@ -926,7 +932,7 @@ knn_status predict_core(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te
     }
     if (c->profile == 2 && gemm) {
         // diagnostic only: total candidates kept by the filter (last pass)
-        std::vector<int32_t> h(std::min(pass, te->n) * 2 * c->stats[2]);
+        std::vector<int32_t> h(std::min(pass, te->n) * c->subs * c->stats[2]);
         if (hipMemcpy(h.data(), c->cnt.p, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost) == hipSuccess) {
             int64_t tot = 0;
             for (int32_t v : h) tot += v;
@@ -1157,7 +1163,7 @@ int32_t knn_stage_times(const knn_ctx* c, const char** names, float* ms, int32_t
 
 int32_t knn_last_stats(const knn_ctx* c, int64_t* out, int32_t n) {
     if (!c || !out) return 0;
-    int32_t m = std::min(n, 9);
+    int32_t m = std::min(n, 10);
     for (int32_t i = 0; i < m; i++) out[i] = c->stats[i];
     return m;
 }

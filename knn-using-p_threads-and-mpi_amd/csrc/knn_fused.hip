@@ -436,6 +436,11 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     // ---- one tile's MFMAs into X; in between, the fast test of the previous tile (Y): a v_min3
     // chain per accumulator; returns bit 16c (x 0xffff) when some lane of accumulator c holds a
     // passing value (the slow path builds the value set, pass_set)
+    [[maybe_unused]] floatx16 cnorm;  // (KNN_ABLATE_NO_NORM only)
+    if constexpr (KNN_STUDY_NO_NORM) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) cnorm[r] = (float)a.d * (1.0f / 3.0f);
+    }
     constexpr int PF = FUSED_PF / NACC;  // k-steps of A fragments read ahead
     uint4 pa[PF], pb[PF];                // PAIR: the odd step's first fragments, read early
     auto prefetch = [&](int buf) __attribute__((always_inline)) {
@@ -458,7 +463,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         // accumulators of a row group share them as the first MFMA's C operand)
         // (the norms land in row group rg's query-group-0 accumulator X[rg]; at k-step 0 the other
         // query groups' MFMAs take them as their C operand first, then X[rg]'s own -- no copy)
-        if constexpr (TN) {
+        if constexpr (TN && !KNN_STUDY_NO_NORM) {
             const unsigned char* hn = tile + HDR + 4 * (4 * h);
 #pragma unroll
             for (int rg = 0; rg < RG; rg++) {
@@ -471,6 +476,11 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                     X[rg][4 * g4 + 3] = v.w;
                 }
             }
+        } else if constexpr (TN) {
+            // (ablation KNN_ABLATE_NO_NORM: every accumulator starts from the mean row norm d/3 of
+            // the uniform generator instead of its rows' norms -- no norm reads; results invalid)
+#pragma unroll
+            for (int rg = 0; rg < RG; rg++) X[rg] = cnorm;
         } else {
 #pragma unroll
             for (int rg = 0; rg < RG; rg++) X[rg] = floatx16{};
@@ -1397,9 +1407,15 @@ FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus, const FusedForc
     // groups so each tile's place is static (pairs -> quads: B 557.2 -> 501.1 ms, A 22.61 ->
     // 21.67 ms, r04i; quads -> octets: A 21.49 -> 20.80 ms, B 504.6 -> 483.8 ms, r04y).
     // force.nbuf = 4|8 forces pairs or quads (a study override).
+    // the v_mfma_f32_16x16x32_bf16 form of a register-list shape (k_gemm_fused16: same tiles,
+    // blocks, LDS image and schedule; a study switch until measured)
+    auto m16 = [&](FilterPlan f) {
+        if (force.m16 && knn_fused16_ptr(d, f)) f.m16 = 1;
+        return f;
+    };
     if (kr > 0 && qg2) {
         const int nb = force.nbuf == 4 || force.nbuf == 8 ? force.nbuf : 16;
-        return make(8, 1, 2, fused_lds_of(rb, k, 8, 1, nb, false, 2) <= cap ? nb : 8, 2);
+        return m16(make(8, 1, 2, fused_lds_of(rb, k, 8, 1, nb, false, 2) <= cap ? nb : 8, 2));
     }
     if (kr == 104) return make(8, 1, 2, 8);
     // list exchange between a query's pieces (a.lshare, knn_capi.cpp): the QG = 1 shapes only
@@ -1411,7 +1427,7 @@ FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus, const FusedForc
         const bool q8 = force.nbuf != 4 && fused_lds_of(rb, k, 8, 2, 8, false) <= cap;
         FilterPlan f = make(8, 2, 2, q8 ? 8 : 4);
         f.ls = 1;
-        return f;
+        return m16(f);
     }
     if (kr == 0 && d == 64 && fused_lds_of(rb, k, 4, 2, 2, true) <= cap / 2) return make(4, 2, 2, 2);
     if (fused_lds_of(rb, k, 8, 2, 4, kr == 0) <= cap) return make(8, 2, 2, 4);
@@ -1450,6 +1466,7 @@ static const void* fused_fn(const FilterPlan& f) {
 }
 
 static const void* fused_ptr(int d, const FilterPlan& f) {
+    if (f.m16) return knn_fused16_ptr(d, f);
     if (d == 64) {
         if constexpr (KNN_FUSED_AUG64) return fused_fn<160>(f);
         else return fused_fn<128>(f);
@@ -1466,6 +1483,7 @@ hipError_t knn_launch_fused(const GemmFilterArgs& a, const FilterPlan& f, hipStr
     const int ld = knn_fused_row_bytes(a.d) / 2;  // operand row pitch in elements
     if (!knn_fused_supported(a.d) || f.nw == 0 || a.ld_t != ld || a.ld_q != ld || !a.qstat)
         return hipErrorInvalidValue;
+    if (f.m16 && !knn_fused16_ptr(a.d, f)) return hipErrorInvalidValue;
     if (f.kr > 0 && !(f.nw == 8 && (((f.nbuf == 4 || f.nbuf == 8) && f.qg == 1 && f.rg == 2 && f.kr <= 32) ||
                                      ((f.nbuf == 4 || f.nbuf == 8 || f.nbuf == 16) && f.qg == 2 && f.rg == 1 && f.kr <= 32) ||
                                      (f.nbuf == 8 && f.qg == 1 && f.rg == 1 && f.kr == 104 && a.d == 256))))

@@ -152,6 +152,7 @@ struct FilterPlan {
     size_t lds;
     int kr = 0;  // fused: register-list shape (16, 32, 104; 0 = LDS heaps)
     int ls = 0;  // fused: the kernel exchanges threshold lists between a query's pieces
+    int m16 = 0;  // fused: the v_mfma_f32_16x16x32_bf16 form of the shape (k_gemm_fused16)
 };
 FilterPlan knn_gemm_filter_plan(int elem, int row_bytes, int k);
 hipError_t knn_launch_gemm_filter(const GemmFilterArgs& a, int elem, int row_bytes, hipStream_t st);
@@ -179,6 +180,7 @@ struct FusedForce {
     int qg = 0;
     int nbuf = 0;
     bool heaps = false;
+    bool m16 = false;  // KNN_FUSED_MFMA16=1: the 16x16x32 form of the register-list shapes (k_gemm_fused16)
 };
 // nw == 0: k too large.  nq, num_cus pick the queries per wave (register-list shapes): 64 on
 // 32-row tiles when the queries fill about 3/4 of a round of 512-query blocks, else 32 on 64-row
@@ -186,6 +188,10 @@ struct FusedForce {
 // operands, the occupancy, the schedule and the launch from that one plan.
 FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus, const FusedForce& force);
 hipError_t knn_fused_occupancy(int d, const FilterPlan& f, int* blocks_per_cu);
+// k_gemm_fused16's kernel for plan f (f.m16; knn_fused16.hip), nullptr if f has no 16x16x32 form
+const void* knn_fused16_ptr(int d, const FilterPlan& f);
+// candidate sub-slices per segment (piece) of plan f: one per lane half (32x32), per quarter (16x16)
+inline int knn_fused_subslices(const FilterPlan& f) { return f.m16 ? 4 : 2; }
 // whether plan f's kernel exchanges threshold lists between a query's pieces (a.lshare, lshare_w floats per piece)
 int knn_fused_list_share_width(const FilterPlan& f);
 // fills a.p1_blocks / g2 / w2 / tiles64 for the balanced schedule over `slots` resident

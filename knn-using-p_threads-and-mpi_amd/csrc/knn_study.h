@@ -23,6 +23,15 @@
 #define KNN_STUDY_NO_DMA 0
 #endif
 
+// KNN_ABLATE_NO_NORM: the fused filter's accumulators start from zero instead of the tile
+// header's norms (no norm ds_read_b128; results invalid) -- prices the norm reads of the
+// 32-query shape (round 6).
+#ifdef KNN_ABLATE_NO_NORM
+#define KNN_STUDY_NO_NORM 1
+#else
+#define KNN_STUDY_NO_NORM 0
+#endif
+
 // KNN_ABLATE_NO_BARRIER: the fused filter's tile barrier keeps its waits but drops the s_barrier
 // (results invalid: waves may read tiles other waves' DMAs have not landed) -- prices the
 // cross-wave synchronisation.
@@ -32,7 +41,7 @@
 #define KNN_STUDY_NO_BARRIER 0
 #endif
 
-#if KNN_STUDY_NO_SLOW || KNN_STUDY_NO_EPI || KNN_STUDY_NO_DMA || KNN_STUDY_NO_BARRIER
+#if KNN_STUDY_NO_SLOW || KNN_STUDY_NO_EPI || KNN_STUDY_NO_DMA || KNN_STUDY_NO_BARRIER || KNN_STUDY_NO_NORM
 // the fallback scan is skipped (results invalid) ...
 #define KNN_STUDY_SKIP_FALLBACK(qlist) \
     do {                               \

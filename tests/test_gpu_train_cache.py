@@ -305,3 +305,33 @@ def test_stream_device_mismatch_rejected(knn):
     finally:
         c.device = 0
         c.close()
+
+
+@pytest.mark.parametrize("dtype,d,k", [("f32", 64, 32), ("f32", 128, 10), ("f32", 128, 16), ("bf16", 64, 24),
+                                       ("f32", 128, 32)])
+def test_fused16_shapes_vs_oracle(knn, oracle, dtype, d, k, monkeypatch):
+    """k_gemm_fused16 (KNN_FUSED_MFMA16=1, round 6): the register-list filter on
+    v_mfma_f32_16x16x32_bf16 -- quarter lists, swizzled LDS rows -- in both query shapes
+    (32 queries per wave on 64-row tiles, 64 on 32-row tiles) gives the oracle's top-k and
+    predictions bit for bit (main.cpp:40-82), the same as the 32x32 filter, and reports its
+    MFMA shape.  Pieces (several per query tile) run the quarter-list exchange."""
+    nt, nq = 21_000 + 37, 1_500 + 11
+    train, labels, test = _rows(knn, nt, nq, d, 31, dtype)
+    trf, lab, tef = train.float().cpu().numpy(), labels.cpu().numpy(), test.float().cpu().numpy()
+    qs = np.linspace(0, nq - 1, 40).astype(np.int64)
+    bad, opred, odist, oidx = oracle.knn(trf, lab, tef[qs], k, 10)
+    assert bad == 0
+    c = knn.Context(0, algo="gemm_bf16")
+    ref = _call(c, train, labels, test, k)
+    c.close()
+    assert ref[3]["filter_mfma"] == 32
+    monkeypatch.setenv("KNN_FUSED_MFMA16", "1")
+    for qg in ("1", "2"):
+        monkeypatch.setenv("KNN_FUSED_QG", qg)
+        c = knn.Context(0, algo="gemm_bf16")
+        got = _call(c, train, labels, test, k)
+        c.close()
+        assert got[3]["fused_norm"] and got[3]["filter_mfma"] == 16, got[3]
+        assert np.array_equal(got[2][qs], oidx) and np.array_equal(got[0][qs], opred)
+        assert np.array_equal(got[1][qs], odist.view(np.uint32))
+        assert _same(got, ref)
