@@ -213,7 +213,7 @@ def bench_arff(args, knn, torch, local):
     assert tf.shape == (nt, d) and qf.shape == (nq, d), (tf.shape, qf.shape)
     C = int(tl.max()) + 1  # train->num_classes() (main.cpp:35)
     dev = torch.device("cuda", local)
-    ctx = knn.Context(local, algo=args.algo, profile=3)  # events around the dominant stages only
+    ctx = knn.Context(local, algo=args.algo, train_splits=args.splits, profile=3)  # events around the dominant stages only
     # device rows are 16-B aligned: [n][ld] with ld = 12 for d = 11 (the pad column is never read)
     ld = (d + 3) // 4 * 4
     train = torch.zeros((nt, ld), dtype=torch.float32, device=dev)
@@ -248,7 +248,8 @@ def bench_arff(args, knn, torch, local):
     pairs = float(nt) * nq * args.steps
     stages = {n: v / args.steps for n, v in stage_sum.items()}
     # the dominant kernel: AUTO picks the direct form here -- k_direct_rows for d <= 16, k <= 16
-    # (config L), else k_direct_tile -- its segments merged by k_merge_vote (stage "merge_vote")
+    # (config L: its segments merged by its own last wave per query group, round 6), else
+    # k_direct_tile -- its segments merged by k_merge_vote (stage "merge_vote")
     kname = "direct_tile" if "direct_tile" in stages else "exact_scan"
     scan = stages.get(kname)
     roof = None

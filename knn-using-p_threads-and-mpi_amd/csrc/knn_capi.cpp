@@ -91,6 +91,9 @@ struct knn_ctx {
     int32_t* ctrl_host = nullptr;  // pinned, mapped, fine-grained: [0] status, [1] fallback count
     int32_t* ctrl_host_dev = nullptr;  // its device address (k_finish writes it)
     bool ctrl_clean = false;  // the status words are zero (the last call ended in k_finish)
+    DBuf arrive;              // k_direct_rows' fused merge: per query group, segments finished
+    bool arrive_clean = false;  // arrive is all zero (the last launch ran to completion)
+    bool merge_kernel = false;  // study switch KNN_DIRECT_MERGE_KERNEL=1: k_direct_rows' segments via k_merge_vote
     // host-buffer calls (knn_predict): cached train upload, two query slots streamed on a copy stream
     int cache_train = 0;
     uint64_t generation = 0;
@@ -255,6 +258,7 @@ knn_status finish_call(knn_ctx* c, hipStream_t st) {
     HIP_OR_FAIL(c, knn_launch_finish(c->ctrl.as<int32_t>(), c->ctrl_host_dev, 4, st));
     HIP_OR_FAIL(c, hipStreamSynchronize(st));
     c->ctrl_clean = true;
+    c->arrive_clean = true;  // every query group's merging wave reset its counter
     collect_stages(c);
     return check_status(c, c->ctrl_host);
 }
@@ -317,6 +321,20 @@ knn_status run_direct_tile(knn_ctx* c, const knn_dataset* tr, const knn_dataset*
     }
     HIP_OR_FAIL(c, c->seg_rec.ensure(sizeof(int32_t) * 3 * (size_t)k * (size_t)te->n * nseg));
     a.rec = c->seg_rec.as<int32_t>();
+    if (knn_direct_rows_shape(k, tr->d) && !c->merge_kernel) {
+        // k_direct_rows merges its segments itself (the last wave of a query group to finish):
+        // one launch, no k_merge_vote pass (config L: 0.012 ms of merge + a launch, round 6)
+        const int64_t groups = knn_direct_rows_groups(te->n);
+        const void* before = c->arrive.p;
+        HIP_OR_FAIL(c, c->arrive.ensure(sizeof(int32_t) * (size_t)groups));
+        if (c->arrive.p != before) c->arrive_clean = false;
+        if (!c->arrive_clean) HIP_OR_FAIL(c, hipMemsetAsync(c->arrive.p, 0, c->arrive.bytes, st));
+        c->arrive_clean = false;  // (set again when the call's stream synchronises)
+        a.arrive = c->arrive.as<int32_t>();
+        a.out = out;
+        HIP_OR_FAIL(c, knn_launch_direct_tile(a, st));
+        return KNN_OK;
+    }
     HIP_OR_FAIL(c, knn_launch_direct_tile(a, st));
     // (the merge is its own stage: "direct_tile" times the distance kernel alone)
     stage_end(c, st);
@@ -735,6 +753,7 @@ knn_status knn_create(knn_ctx** out, const knn_opts* opts) {
     c->no_lshare = getenv("KNN_NO_LIST_SHARE") != nullptr;
     c->no_cursor = getenv("KNN_NO_SCAN_CURSOR") != nullptr;
     c->rescore_all = getenv("KNN_RESCORE_ALL") != nullptr;
+    c->merge_kernel = getenv("KNN_DIRECT_MERGE_KERNEL") != nullptr;
     if (c->device < 0 || c->device >= ndev) { delete c; return KNN_ENODEV; }
     hipDeviceProp_t prop;
     if (hipSetDevice(c->device) != hipSuccess || hipGetDeviceProperties(&prop, c->device) != hipSuccess) {
@@ -778,7 +797,7 @@ void knn_destroy(knn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (DBuf* b : {&c->tnorm, &c->tnp, &c->qnorm, &c->gthr, &c->cnt, &c->cand,
-                    &c->fb_list, &c->ctrl, &c->scratch, &c->split_t, &c->split_q, &c->pad_t, &c->seg_rec, &c->tmax, &c->qstat, &c->tblk, &c->tctrl, &c->cursor, &c->lshare, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
+                    &c->fb_list, &c->ctrl, &c->scratch, &c->split_t, &c->split_q, &c->pad_t, &c->seg_rec, &c->arrive, &c->tmax, &c->qstat, &c->tblk, &c->tctrl, &c->cursor, &c->lshare, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
                     &c->h_dist, &c->h_idx})
         b->release();
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);

@@ -913,6 +913,21 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             }
         }
     };
+    // a kept row into this lane's list and candidate sub-slice (register lists).  (Round 6: these
+    // inserts deferred -- kept rows queued two per lane, flushed for all lanes together every
+    // 16 / 64 tiles or when a queue filled -- measured A 19.59 -> 19.98 / 19.65 ms, B 469.8 ->
+    // 471.2, A's 8-GPU share equal, same box, r06l: the sparse late visits' cost is the lane
+    // scan and its latency, not the insert)
+    auto keep_row = [&](int g, bool keep, float L, float U, int64_t t) __attribute__((always_inline)) {
+        if constexpr (RL) {
+            if (keep) store_cand(g, L, U, t);
+            const float w = (keep && U < lst[g][LL - 1]) ? U : INF;
+            if (__ballot(w < INF)) {
+                list_insert(g, w);
+                thr[g] = fmin_op(thr[g], __builtin_amdgcn_fmed3f(lst[g][LL - 1], partner(lst[g][LL - 1]), INF));
+            }
+        }
+    };
     auto slow_rl = [&](floatx16 (&Y)[NACC], int tp, const float (&tf)[QG], const TQ& tq, const float (&mnY)[NACC],
                        uint32_t u) {
         if constexpr (RL) {
@@ -925,13 +940,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
                 const int64_t t = tbase + row;
                 float L, U;
                 bounds(g, yv, tq.v[g], L, U);
-                const bool keep = idx >= 0 && t < row_end && L <= thr[g];
-                if (keep) store_cand(g, L, U, t);
-                const float w = (keep && U < lst[g][LL - 1]) ? U : INF;
-                if (__ballot(w < INF)) {
-                    list_insert(g, w);
-                    thr[g] = fmin_op(thr[g], __builtin_amdgcn_fmed3f(lst[g][LL - 1], partner(lst[g][LL - 1]), INF));
-                }
+                keep_row(g, idx >= 0 && t < row_end && L <= thr[g], L, U, t);
             };
             lane_rounds(Y, tf, mnY, u, visit);
 #pragma unroll

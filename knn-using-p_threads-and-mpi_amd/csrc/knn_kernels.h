@@ -113,6 +113,10 @@ struct DirectTileArgs {
     int vote_lds;              // per-wave LDS class counts (C <= KNN_VOTE_LDS_MAX_C)
     QueryOut out; int32_t* status;
     int32_t* rec;              // nseg > 1: segment records [nseg][nq][3][k] (local rows)
+    // k_direct_rows with nseg > 1 (optional): per query group, the segments that finished
+    // (zero between calls); the last wave of a group merges every segment's records and votes
+    // in the same launch (no k_merge_vote pass)
+    int32_t* arrive;
 };
 // queries per k_direct_tile block for k (8 * QW, QW = max(1, 8 / list registers))
 int knn_direct_tile_qb(int k);
@@ -125,6 +129,9 @@ hipError_t knn_direct_units(int k, int elem, int d, int C, int* queries_per_unit
 // fills dc / stride / vote_lds / n_qblocks from d, C, nq and launches nseg units per query
 // unit (k_direct_tile: blocks; k_direct_rows for d <= 16, k <= 16: waves, four per block)
 hipError_t knn_launch_direct_tile(DirectTileArgs a, hipStream_t st);
+// whether (k, d) runs k_direct_rows (d <= 16, k <= 16), and its query groups for nq queries
+bool knn_direct_rows_shape(int k, int d);
+int64_t knn_direct_rows_groups(int64_t nq);
 
 struct GenerateArgs {
     void* out; int32_t* labels; int64_t row0; int64_t n; int d; int ld;

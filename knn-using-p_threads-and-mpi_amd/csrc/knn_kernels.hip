@@ -529,6 +529,12 @@ __global__ __launch_bounds__(64 * DT_NW, 4) void k_direct_tile(DirectTileArgs a)
 // u / n_qb, so the waves one CU runs at once share a segment's rows in L2.
 // ---------------------------------------------------------------------------------
 typedef float f2v __attribute__((ext_vector_type(2)));
+// the wave list T (one register) merged with a batch of 64 keys, one copy of the network
+__device__ __attribute__((noinline)) u64 merge_tile_keys(u64 T, u64 x) {
+    u64 t[1] = {T};
+    topk_merge<1>(t, x);
+    return t[0];
+}
 template <int NG, int QW, typename E>
 __global__ __launch_bounds__(256) void k_direct_rows(DirectTileArgs a) {
     static_assert(QW % 2 == 0, "queries go in pairs");
@@ -627,8 +633,12 @@ __global__ __launch_bounds__(256) void k_direct_rows(DirectTileArgs a) {
                 // many passing rows (train rows in decreasing distance order, e.g. sorted or
                 // clustered data): one bitonic merge of the tile instead of up to 64 serial lane
                 // shifts -- k_direct_tile's SH guard.  Same result: the merge keeps the
-                // k smallest (distance, index) keys, the shifts insert in row order
-                topk_merge<1>(T[i], pass ? make_key(di, (uint32_t)row) : KEY_NONE);
+                // k smallest (distance, index) keys, the shifts insert in row order.  Out of line:
+                // inlined in the loop's six tile copies it cost config L 17 % (r06i); out of line
+                // 7 % (0.083 -> 0.089 ms, 61 -> 65 VGPRs; bounding the kernel to 64 VGPRs spilled:
+                // 0.115 ms, r06l), while train rows in decreasing distance ran 16x slower than
+                // uniform rows without it and 6x with it (scripts/diag_direct_rows_adversarial.py)
+                T[i][0] = merge_tile_keys(T[i][0], pass ? make_key(di, (uint32_t)row) : KEY_NONE);
                 thr[i] = kth_dist(T[i][0], k);
                 m = 0;
             }
@@ -666,6 +676,21 @@ __global__ __launch_bounds__(256) void k_direct_rows(DirectTileArgs a) {
             if (qi[i] < a.nq) finish_query<1>(T[i], k, a.C, a.labels, nullptr, qi[i], a.out, a.status);
         return;
     }
+    // Fused merge (round 6, a.arrive): the last of the query group's nseg waves to finish merges
+    // every segment's records into its own list -- by (distance, row): the reference's
+    // lower-index tie rule across segments, as k_merge_vote -- and votes, in this launch.  The
+    // records cross CUs (and XCDs, whose L2s are not coherent with each other) inside the
+    // kernel, so they go through device-scope (sc1) stores and loads, which the XCD L2s do not
+    // hold stale; `s_waitcnt vmcnt(0)` retires this wave's record stores before lane 0's
+    // device-scope arrival, and the last arriver reads the others' records only after it saw
+    // the count.  (An agent-scope release / acquire fence would add an L2 write-back and
+    // invalidate per wave: buffer_wbl2 / buffer_inv sc1.)  The merging wave resets the
+    // group's counter: zero between calls.
+    const bool fused = a.arrive != nullptr;
+    auto put = [&](int32_t* p, int32_t v) __attribute__((always_inline)) {
+        if (fused) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else *p = v;
+    };
 #pragma unroll
     for (int i = 0; i < QW; i++) {
         if (qi[i] >= a.nq) continue;
@@ -674,10 +699,38 @@ __global__ __launch_bounds__(256) void k_direct_rows(DirectTileArgs a) {
             const u64 key = T[i][0];
             const bool none = key == KEY_NONE;
             const int32_t idx = (int32_t)(uint32_t)(key & 0xffffffffull);
-            rec[lane] = none ? (int32_t)__float_as_uint(FLT_MAX) : (int32_t)(uint32_t)(key >> 32);
-            rec[k + lane] = none ? -1 : idx;
-            rec[2 * k + lane] = none ? -1 : a.labels[idx];
+            put(rec + lane, none ? (int32_t)__float_as_uint(FLT_MAX) : (int32_t)(uint32_t)(key >> 32));
+            put(rec + k + lane, none ? -1 : idx);
+            put(rec + 2 * k + lane, none ? -1 : a.labels[idx]);
         }
+    }
+    if (!fused) return;  // (k_merge_vote merges the segments)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(&a.arrive[qg], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != a.nseg - 1) return;
+    if (lane == 0) __hip_atomic_store(&a.arrive[qg], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int i = 0; i < QW; i++) {
+        if (qi[i] >= a.nq) continue;
+        u64 kth = list_at(T[i], k - 1);
+        for (int s = 0; s < a.nseg; s++) {
+            if (s == seg) continue;  // (this wave's own list is T[i] already)
+            const int32_t* rec = a.rec + ((int64_t)s * a.nq + qi[i]) * 3 * (int64_t)k;
+            u64 key = KEY_NONE;
+            if (lane < k) {
+                const int32_t ix = __hip_atomic_load(rec + k + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int32_t db = __hip_atomic_load(rec + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (ix >= 0) key = make_key(__int_as_float(db), (uint32_t)ix);
+            }
+            // a segment's list ascends: the keys below the current k-th are its prefix
+            const bool pass = key < kth;
+            if (!__ballot(pass)) continue;
+            topk_merge_sorted<1>(T[i], pass ? key : KEY_NONE);
+            kth = list_at(T[i], k - 1);
+        }
+        finish_query<1>(T[i], k, a.C, a.labels, nullptr, qi[i], a.out, a.status);
     }
 }
 #pragma clang fp contract(on)
@@ -2152,6 +2205,8 @@ static const void* direct_tile_ptr(int k, int elem) {
 #endif
 static constexpr int DR_QW = KNN_DR_QW;
 static bool direct_rows(int k, int d) { return d <= 16 && k <= 16; }
+bool knn_direct_rows_shape(int k, int d) { return direct_rows(k, d); }
+int64_t knn_direct_rows_groups(int64_t nq) { return (nq + DR_QW - 1) / DR_QW; }
 template <typename E>
 static const void* direct_rows_fn(int d) {
     switch ((d + 3) / 4) {
