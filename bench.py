@@ -267,6 +267,8 @@ def bench_arff(args, knn, torch, local):
                               "(v_pk_add/mul_f32: two ops per lane) -- MI355X_MICROARCH.md: 157.3 TFLOP/s "
                               "counting an FMA as 2",
                 "merge_ms": round(stages.get("merge_vote", 0.0), 4),
+                "merge": ("fused: each query group's last segment wave merges + votes (round 6)"
+                          if kernel == "k_direct_rows" else "k_merge_vote"),
                 "note": "launch/latency bound: 52.9 M pairs is ~22 us of VALU at peak"}
     out = {
         "metric": METRIC, "value": pairs / elapsed, "unit": "pairs/s", "n_gpus": 1,
