@@ -67,7 +67,8 @@ done
 
 for cfg in $PROFILE; do
   st=2; [ "$cfg" != A ] && st=1; [ "$cfg" = L ] && st=50
-  STEPS=$st PROF_TAG=${TAG}_$cfg BENCH_ARGS="--config $cfg ${PROFILE_ARGS:-}" bash scripts/profile_bench.sh || exit 1
+  tst=$st; [ "$cfg" = A ] && tst=100; [ "$cfg" = B ] && tst=5; [ "$cfg" = L ] && tst=300
+  TRACE_STEPS=$tst STEPS=$st PROF_TAG=${TAG}_$cfg BENCH_ARGS="--config $cfg ${PROFILE_ARGS:-}" bash scripts/profile_bench.sh || exit 1
 done
 
 if [ "$SMOKE" = 1 ]; then

@@ -16,8 +16,11 @@ OUT=$R/gpurun_out
 PT=${PROF_TAG:-prof}   # output dirs $OUT/${PT}_{trace,fetch,write,sq}
 BENCH="$R/bench.py --steps $STEPS --warmup 1 --no-cpu-baseline --no-host-path --no-bit-match --no-uncached ${BENCH_ARGS:-}"
 
+# (the trace pass runs TRACE_STEPS timed steps: a 2-step run averages the first launches, whose clock
+# differs -- A: 20.15 ms over 2 steps, 19.19 ms over 100 against the bench's 19.2-19.5 by events, r06x)
+TBENCH="$R/bench.py --steps ${TRACE_STEPS:-$STEPS} --warmup 1 --no-cpu-baseline --no-host-path --no-bit-match --no-uncached ${BENCH_ARGS:-}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${PT}_trace -o run \
-    -- python3 $BENCH > $OUT/${PT}_trace.log 2>&1 || { echo "trace pass failed"; exit 1; }
+    -- python3 $TBENCH > $OUT/${PT}_trace.log 2>&1 || { echo "trace pass failed"; exit 1; }
 echo "trace pass ok"
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/${PT}_fetch -o run \
     -- python3 $BENCH > $OUT/${PT}_fetch.log 2>&1 || { echo "fetch pass failed"; exit 1; }
