@@ -63,6 +63,7 @@ struct knn_ctx {
     DBuf pad_t;             // KNN_ALGO_GEMM, n_train not a multiple of 64: the rows padded to the tile grid
     DBuf seg_rec;           // k_direct_tile segment records [nseg][nq][3][k]
     DBuf tmax;              // fused filter: per-64-row train stats {max tn, max |t - rt|, max |rt|, 0}
+    DBuf tsmax;             // fused filter: their maxima over all tiles (k_tile_stat_max; cached with tmax)
     DBuf cursor;            // fused filter: per-XCD scan cursors (64-row units; performance hint only)
     DBuf lshare;            // fused filter: per (query, piece) threshold lists shared between pieces
     DBuf qstat;             // fused filter: per-query {|q|, |q - rq|} upper bounds
@@ -492,6 +493,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     if (fused) {
         certificate_fused(d, felem == ELEM_ROUND, &coef, &eta);
         HIP_OR_FAIL(c, c->tmax.ensure(sizeof(float4) * ((nt + 63) / 64 + 1)));
+        HIP_OR_FAIL(c, c->tsmax.ensure(sizeof(float4)));
         HIP_OR_FAIL(c, c->qstat.ensure(sizeof(float2) * (nq + 1)));
     } else {
         certificate(d, felem, &coef, &eta);
@@ -522,6 +524,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
             HIP_OR_FAIL(c, knn_launch_row_norms(tr->feat, dtype, nt, tr->ld, d, c->tnorm.as<float>(),
                                                 c->tctrl.as<int32_t>(), c->tctrl.as<uint32_t>() + 2,
                                                 c->tnp.as<float>(), 1.0f - coef, st, c->tmax.as<float4>(), nullptr));
+            HIP_OR_FAIL(c, knn_launch_tile_stat_max(c->tmax.as<float4>(), (nt + 63) / 64, c->tsmax.as<float4>(), st));
         }
         HIP_OR_FAIL(c, hipMemcpyAsync(c->ctrl.p, c->tctrl.p, 4 * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     } else {
@@ -529,6 +532,8 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
                                             c->ctrl.as<int32_t>(), c->ctrl.as<uint32_t>() + 2,
                                             c->tnp.as<float>(), 1.0f - coef, st, fused ? c->tmax.as<float4>() : nullptr,
                                             gate));
+        if (fused && !gate)
+            HIP_OR_FAIL(c, knn_launch_tile_stat_max(c->tmax.as<float4>(), (nt + 63) / 64, c->tsmax.as<float4>(), st));
     }
     // (the fused filter's query operand is rn(-2 q): its rounding is bounded for rn(-2 q) / -2)
     HIP_OR_FAIL(c, knn_launch_row_norms(te->feat, dtype, nq, te->ld, d, c->qnorm.as<float>(),
@@ -655,6 +660,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     g.gthr = c->gthr.as<uint32_t>();
     g.cnt = c->cnt.as<int32_t>(); g.cand = c->cand.as<CandRec>(); g.cap = cap; g.cap_seg = cap / nseg;
     g.qstat = fused ? c->qstat.as<float2>() : nullptr;
+    g.tsmax = fused ? c->tsmax.as<float4>() : nullptr;
     // per-XCD scan cursors for the multi-segment schedule (B: filter traffic beyond L2 664 ->
     // 494 GB per launch, time unchanged; with one segment or the balanced schedule they saved
     // nothing: r03s).  KNN_NO_SCAN_CURSOR=1 turns them off (a diagnostic; same results).
@@ -797,7 +803,7 @@ void knn_destroy(knn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (DBuf* b : {&c->tnorm, &c->tnp, &c->qnorm, &c->gthr, &c->cnt, &c->cand,
-                    &c->fb_list, &c->ctrl, &c->scratch, &c->split_t, &c->split_q, &c->pad_t, &c->seg_rec, &c->arrive, &c->tmax, &c->qstat, &c->tblk, &c->tctrl, &c->cursor, &c->lshare, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
+                    &c->fb_list, &c->ctrl, &c->scratch, &c->split_t, &c->split_q, &c->pad_t, &c->seg_rec, &c->arrive, &c->tmax, &c->tsmax, &c->qstat, &c->tblk, &c->tctrl, &c->cursor, &c->lshare, &c->h_train, &c->h_labels, &c->h_test, &c->h_pred,
                     &c->h_dist, &c->h_idx})
         b->release();
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);

@@ -42,6 +42,9 @@ static constexpr int FUSED_RQ = 4;            // queued passing values per lane 
 #ifndef KNN_FUSED_LIST_FIRST
 #define KNN_FUSED_LIST_FIRST 31               // first list exchange after this tile (then doubling)
 #endif
+#ifndef KNN_FUSED_TF_GLOBAL
+#define KNN_FUSED_TF_GLOBAL 1                 // fast-test tile term from the maxima over all tiles (a.tsmax)
+#endif
 #ifndef KNN_FUSED_DMA_FRONT
 #define KNN_FUSED_DMA_FRONT 0                 // (study) a group's tile DMAs all issued right after its barrier
 #endif
@@ -192,6 +195,37 @@ hipError_t knn_launch_tn_rows(const void* x, int elem, int64_t n, int64_t n_vali
 }
 
 // ---------------------------------------------------------------------------------
+// k_tile_stat_max: out = {max tn, max |t - rt|, max |rt|, 0} over the n 64-row tile statistics
+// (k_row_norms' tstat): the fused filter's fast-test tile term (a.tsmax).  One block.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_tile_stat_max(const float4* __restrict__ t, int64_t n, float4* __restrict__ out) {
+    __shared__ float4 part[4];
+    float4 m = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // (the statistics are >= 0)
+    for (int64_t i = threadIdx.x; i < n; i += 256) {
+        const float4 v = t[i];
+        m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        m.x = fmaxf(m.x, __shfl_xor(m.x, o)); m.y = fmaxf(m.y, __shfl_xor(m.y, o)); m.z = fmaxf(m.z, __shfl_xor(m.z, o));
+    }
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float4 r = part[0];
+        for (int w = 1; w < 4; w++) { r.x = fmaxf(r.x, part[w].x); r.y = fmaxf(r.y, part[w].y); r.z = fmaxf(r.z, part[w].z); }
+        *out = r;
+    }
+}
+
+hipError_t knn_launch_tile_stat_max(const float4* tstat, int64_t n, float4* out, hipStream_t st) {
+    if (n <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_tile_stat_max, dim3(1), dim3(256), 0, st, tstat, n, out);
+    KNN_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------------
 // k_gemm_fused<RB, MINW, NBUF, NW, RG>: the filter (RB = bytes per augmented row,
 // 2d + 32).  Block = NW waves x 32 queries; a train tile has BN = 32 RG rows, copied
 // global -> LDS by LDS-DMA (NBUF buffers, one barrier per tile, pieces issued between
@@ -312,17 +346,6 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         ccnt[g] = 0;
     }
     float root = INF;  // (heap shapes, QG = 1) this query's heap root, mirrored in both lanes
-    float tfb[QG];     // tf without the tile term
-    auto make_tfb = [&](int g) __attribute__((always_inline)) {
-        tfb[g] = qvalid[g] ? ((thr[g] - qn[g]) + fmaf(coef, qn[g], eta)) + 0x1p-18f * (fabsf(thr[g]) + qn[g]) : -INF;
-    };
-#pragma unroll
-    for (int g = 0; g < QG; g++) make_tfb(g);
-    // tile term: tq = {the tile's maximum norm tmax, the operand-rounding bound of this query
-    // against the tile's rows, 2 (|q| max|t - rt| + |q - rq| max|rt|) (1 + 2^-17)}
-    auto tf_of = [&](int g, float2 tq) __attribute__((always_inline)) {
-        return fmaf(coef + 0x1p-18f, tq.x, tfb[g]) + tq.y;
-    };
     float qe2[QG], eq2[QG];  // 2 |q| and 2 |q - rq|, rounded up
 #pragma unroll
     for (int g = 0; g < QG; g++) {
@@ -333,6 +356,34 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             eq2[g] = 2.0f * qs.y * (1.0f + 0x1p-17f);
         }
     }
+    // Fast-test tile term (round 6, TFG): from the maxima over ALL tiles of the tile statistics
+    // (a.tsmax = {max tn, max |t - rt|, max |rt|} over the train set's 64-row tiles) instead of
+    // each tile's own: one threshold tfc per query group, rebuilt only when the threshold moves
+    // (make_tfb) -- no header read and two FMAs per group and tile.  The maxima bound every
+    // tile's, so the test passes a superset of what the per-tile test passed (the 2^-18 slack
+    // covers the reordered additions); the slow path still bounds L, U with the tile's own
+    // statistics, read when it runs (the tile's buffer is not rewritten before the next group's
+    // DMA: PAIR shapes, AHEAD = GRP).  On uniform rows the tile maxima vary by a few 1e-4 of the
+    // band.  KNN_FUSED_TF_GLOBAL=0: the per-tile term (round 5).
+    constexpr bool TFG = KNN_FUSED_TF_GLOBAL && PAIR && TN;
+    float tk[QG], tfc[QG];  // (TFG) the tile term and the fast-test threshold, per query group
+    if constexpr (TFG) {
+        const float4 smax = *a.tsmax;
+#pragma unroll
+        for (int g = 0; g < QG; g++) tk[g] = fmaf(coef + 0x1p-18f, smax.x, fmaf(qe2[g], smax.y, eq2[g] * smax.z));
+    }
+    float tfb[QG];     // tf without the tile term
+    auto make_tfb = [&](int g) __attribute__((always_inline)) {
+        tfb[g] = qvalid[g] ? ((thr[g] - qn[g]) + fmaf(coef, qn[g], eta)) + 0x1p-18f * (fabsf(thr[g]) + qn[g]) : -INF;
+        if constexpr (TFG) tfc[g] = tfb[g] + tk[g];
+    };
+#pragma unroll
+    for (int g = 0; g < QG; g++) make_tfb(g);
+    // tile term: tq = {the tile's maximum norm tmax, the operand-rounding bound of this query
+    // against the tile's rows, 2 (|q| max|t - rt| + |q - rq| max|rt|) (1 + 2^-17)}
+    auto tf_of = [&](int g, float2 tq) __attribute__((always_inline)) {
+        return fmaf(coef + 0x1p-18f, tq.x, tfb[g]) + tq.y;
+    };
     // the tile's statistics, from its LDS image (TN: the header's last slot, fp32; the
     // KNN_STUDY_AUG64 layout: augmented columns d+8..d+10 of row 0, bf16): one broadcast read,
     // in order with the fragment reads -- no scalar memory load in the loop
@@ -1133,7 +1184,8 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         const uint64_t t1 = now();
         // this tile's terms, for its fast test in the next iteration (the tile is resident:
         // landed before this step's barrier, not overwritten before the next one)
-        const TQ tm_cur = tile_q(it % NBUF);
+        TQ tm_cur;
+        if constexpr (!TFG) tm_cur = tile_q(it % NBUF);
         // Tile DMAs.  Spread (the round-4 order): step it issues tile it + AHEAD's pieces between
         // its MFMAs -- so the next group's last tile goes out in the last step before the
         // barrier that waits for it (vmcnt(0)), and its whole memory latency is exposed at every
@@ -1161,7 +1213,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         const DmaTile dd = dma_desc((it + AHEAD) % NBUF, it + AHEAD);
         float tf[QG];
 #pragma unroll
-        for (int g = 0; g < QG; g++) tf[g] = it > 0 ? tf_of(g, tm_prev.v[g]) : -INF;
+        for (int g = 0; g < QG; g++) tf[g] = it > 0 ? (TFG ? tfc[g] : tf_of(g, tm_prev.v[g])) : -INF;
         float mnY[NACC];
         const uint32_t uY = step(X, Y, it % NBUF, dma_on, dd, tf, POS != 0, mnY);
         // PAIR: the pair's next tile is resident since its barrier -- its first fragments are
@@ -1170,9 +1222,11 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         const uint64_t t2 = now();
         if (!KNN_STUDY_NO_SLOW) {
             if (uY) {
-                if constexpr (RL) slow_rl(Y, it - 1, tf, tm_prev, mnY, uY);
-                else if constexpr (DEFER) record(Y, it - 1, tf[0], tm_prev.v[0], uY);
-                else slow(Y, it - 1, tf[0], tm_prev.v[0], uY);
+                // (TFG: the previous tile's own statistics, for the bounds, from its buffer now)
+                const TQ tq = TFG ? tile_q((it - 1) % NBUF) : tm_prev;
+                if constexpr (RL) slow_rl(Y, it - 1, tf, tq, mnY, uY);
+                else if constexpr (DEFER) record(Y, it - 1, tf[0], tq.v[0], uY);
+                else slow(Y, it - 1, tf[0], tq.v[0], uY);
             }
             if constexpr (DEFER) {
                 if ((it & (FUSED_DEFER_EVERY - 1)) == FUSED_DEFER_EVERY - 1 && __ballot(qcnt > 0)) flush();
@@ -1187,7 +1241,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             st_slow += t3 - t2;
             st_visits += uY ? 1 : 0;
         }
-        tm_prev = tm_cur;
+        if constexpr (!TFG) tm_prev = tm_cur;
     };
     typedef std::integral_constant<int, 0> P0;
     typedef std::integral_constant<int, 1 % GRP> P1;
@@ -1218,9 +1272,10 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     if (ntiles > 0) {
         // drain: the last tile's accumulators (ntiles is even: accB)
         const int last = ntiles - 1;
+        if constexpr (TFG) tm_prev = tile_q(last % NBUF);  // (no DMA since: the buffer holds it)
         float tf[QG];
 #pragma unroll
-        for (int g = 0; g < QG; g++) tf[g] = tf_of(g, tm_prev.v[g]);
+        for (int g = 0; g < QG; g++) tf[g] = TFG ? tfc[g] : tf_of(g, tm_prev.v[g]);
         if constexpr (RL) {
             float mnB[NACC];
 #pragma unroll

@@ -61,6 +61,9 @@ struct GemmFilterArgs {
     // fused filter, register-list shapes with nseg > 1 (optional): each piece's threshold list
     // [nq][nseg][lshare_w] (U values, +inf where empty), shared between a query's pieces
     float* lshare; int lshare_w;
+    // fused filter: the maxima over all 64-row tiles of the tile statistics {max tn, max |t - rt|,
+    // max |rt|, 0} (k_tile_stat_max): the fast test's tile term, one per query group and piece
+    const float4* tsmax;
     const int32_t* status;  // the call's status word: a set GEMM_UNSAFE bit skips the filter
     const int32_t* gate;    // optional: the filter runs only when *gate != 0 (AUTO's re-run)
 };
@@ -195,6 +198,8 @@ struct FusedForce {
 // operands, the occupancy, the schedule and the launch from that one plan.
 FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus, const FusedForce& force);
 hipError_t knn_fused_occupancy(int d, const FilterPlan& f, int* blocks_per_cu);
+// out = component maxima of n tile statistics (the fused filter's a.tsmax)
+hipError_t knn_launch_tile_stat_max(const float4* tstat, int64_t n, float4* out, hipStream_t st);
 // k_gemm_fused16's kernel for plan f (f.m16; knn_fused16.hip), nullptr if f has no 16x16x32 form
 const void* knn_fused16_ptr(int d, const FilterPlan& f);
 // candidate sub-slices per segment (piece) of plan f: one per lane half (32x32), per quarter (16x16)
