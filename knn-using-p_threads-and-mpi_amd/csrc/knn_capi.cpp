@@ -487,7 +487,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     // bf16 MFMA operands (rounded fp32 rows or bf16 data) run the fused-norm filter
     // the fused filter's plan, computed once: it sizes the tile blocks (bn_f), the occupancy,
     // the schedule and the launch of this pass
-    const FilterPlan fplan = knn_fused_supported(d) ? knn_fused_plan(d, k, nq, c->num_cus, c->fforce) : FilterPlan{};
+    const FilterPlan fplan = knn_fused_supported(d) ? knn_fused_plan(d, k, nq, c->num_cus, c->fforce, max_splits(nt, k, cap)) : FilterPlan{};
     const bool fused = (felem == ELEM_ROUND || felem == ELEM_BF16) && knn_fused_supported(d) && fplan.nw > 0;
     float coef, eta;
     if (fused) {

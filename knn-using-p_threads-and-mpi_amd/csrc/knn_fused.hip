@@ -1444,7 +1444,7 @@ int knn_fused_row_bytes(int d) { return d == 64 && KNN_FUSED_AUG64 ? 2 * d + 32 
 //    8-wave blocks: pairs when they fit beside the heaps, else two buffers, else 32-row tiles.
 // Register lists, one per lane half: k <= 16 8 entries (KR = 8), k <= 32 16 (KR = 32: exact
 // 32-entry lists cost a block per CU of occupancy and 9 % of time on B).
-FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus, const FusedForce& force) {
+FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus, const FusedForce& force, int max_pieces) {
     const int rb = knn_fused_row_bytes(d);
     const size_t cap = 160 * 1024 - 256;  // room for the kernel's static LDS
     // d = 256, 32 < k <= 104 (C): per-half 52-entry register lists instead of LDS heaps, so
@@ -1460,13 +1460,21 @@ FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus, const FusedForc
     // Register-list shapes: 64 queries per wave on 32-row tiles (QG = 2: each A fragment read
     // from LDS feeds two MFMAs, the two accumulators share one norm read, and each tile copy
     // serves 512 queries -- half the LDS reads and DMA per MFMA) when the 512-query blocks fill
-    // about 3/4 of a round of CUs; fewer queries would cut each query tile into many pieces
-    // (each piece starts its thresholds from +inf), so they keep 32 per wave on 64-row tiles.
-    // Same box (profiles/r04c): A 24.08 -> 23.19 ms, B 575.9 -> 550.9 ms; A's 8-GPU share
-    // (12,500 queries) 3.40 -> 6.33 ms with QG = 2, hence the rule.
+    // a round of CUs: at least 384 queries per CU, or (round 6) when the query tiles times the
+    // most pieces a query's candidate list allows (max_pieces, the caller's capacity rule)
+    // reach 80 % of the CUs (one such block per CU: 8 waves at ~240 VGPRs).  Fewer queries
+    // would leave CUs idle (pieces beyond max_pieces overflow the lists) or cut each query
+    // tile into many pieces (each piece starts its thresholds from +inf), so they keep 32 per
+    // wave on 64-row tiles (with the list exchange).  Same box (profiles/r04c): A 24.08 -> 23.19
+    // ms, B 575.9 -> 550.9 ms; A's 8-GPU share (12,500 queries) 3.40 -> 6.33 ms with QG = 2.
+    // The fill rule (profiles/r06_studies/r06qg, r06qh; filter ms, QG = 1 -> 2, A's rows, d and
+    // k): 18,750 queries (37 tiles x 5 pieces = 71 % of the CUs) 4.57 -> 4.83, 21,875 (84 %)
+    // 5.21 -> 5.02, 25,000 5.73 -> 5.19, 50,000 11.02 -> 10.10, 75,000 16.49 -> 14.50, 90,000
+    // 18.27 -> 16.83; B's rows (2 pieces): 31,250 (48 %) 17.2 -> 29.1, 62,500 (96 %) 31.9 -> 30.7.
     // force.qg = 1|2 forces the choice (a study override, snapshot at knn_create).
     // (d = 256 keeps 32 queries per wave: two query groups' operands alone are 128 VGPRs)
-    const bool qg2 = d <= 128 && (force.qg == 2 || (force.qg != 1 && nq >= (int64_t)384 * num_cus));
+    const bool fills = (nq + 511) / 512 * (int64_t)std::max(max_pieces, 1) * 5 >= (int64_t)4 * num_cus;
+    const bool qg2 = d <= 128 && (force.qg == 2 || (force.qg != 1 && (nq >= (int64_t)384 * num_cus || fills)));
     // tiles in octets: 16 buffers, one barrier per eight 32-row tiles, the loop running whole
     // groups so each tile's place is static (pairs -> quads: B 557.2 -> 501.1 ms, A 22.61 ->
     // 21.67 ms, r04i; quads -> octets: A 21.49 -> 20.80 ms, B 504.6 -> 483.8 ms, r04y).

@@ -192,11 +192,12 @@ struct FusedForce {
     bool heaps = false;
     bool m16 = false;  // KNN_FUSED_MFMA16=1: the 16x16x32 form of the register-list shapes (k_gemm_fused16)
 };
-// nw == 0: k too large.  nq, num_cus pick the queries per wave (register-list shapes): 64 on
-// 32-row tiles when the queries fill about 3/4 of a round of 512-query blocks, else 32 on 64-row
-// tiles (fewer pieces per query tile).  run_gemm computes the plan once per pass and sizes the
+// nw == 0: k too large.  nq, num_cus and max_pieces (the most pieces a query's candidate list
+// allows) pick the queries per wave (register-list shapes): 64 on 32-row tiles when the
+// 512-query blocks, at most max_pieces per query tile, fill 80 % of a round of CUs, else 32 on
+// 64-row tiles (fewer pieces per query tile).  run_gemm computes the plan once per pass and sizes the
 // operands, the occupancy, the schedule and the launch from that one plan.
-FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus, const FusedForce& force);
+FilterPlan knn_fused_plan(int d, int k, int64_t nq, int num_cus, const FusedForce& force, int max_pieces);
 hipError_t knn_fused_occupancy(int d, const FilterPlan& f, int* blocks_per_cu);
 // out = component maxima of n tile statistics (the fused filter's a.tsmax)
 hipError_t knn_launch_tile_stat_max(const float4* tstat, int64_t n, float4* out, hipStream_t st);
