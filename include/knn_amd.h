@@ -268,7 +268,9 @@ int32_t knn_stage_times(const knn_ctx* ctx, const char** names, float* ms, int32
  * bytes and [7] query bytes a knn_predict call copied host -> device, [8] 1 when the
  * filter's train-side operands came from the KNN_OPT_CACHE_TRAIN cache (no train norm or
  * tile-block pass ran), [9] the fused filter's MFMA shape (32: v_mfma_f32_32x32x16_bf16,
- * 16: v_mfma_f32_16x16x32_bf16, 0: no fused filter ran).  Returns the number written (<= 10). */
+ * 16: v_mfma_f32_16x16x32_bf16, 0: no fused filter ran), [10] the fused filter's queries per
+ * wave (32 or 64, knn_fused_plan's rule; 0: no fused filter ran).  Returns the number
+ * written (<= 11). */
 int32_t knn_last_stats(const knn_ctx* ctx, int64_t* out, int32_t n);
 
 /*

@@ -500,12 +500,13 @@ class Context:
         return out
 
     def stats(self):
-        v = (ctypes.c_int64 * 10)()
-        self.lib.knn_last_stats(self.h, v, 10)
+        v = (ctypes.c_int64 * 11)()
+        self.lib.knn_last_stats(self.h, v, 11)
         return {"candidates": v[0], "fallback_queries": v[1], "train_segments": v[2],
                 "filter_operands": FILTER_OPERANDS.get(v[3], v[3]), "rerun_split": bool(v[4]),
                 "fused_norm": bool(v[5]), "h2d_train_bytes": v[6], "h2d_query_bytes": v[7],
-                "train_operands_cached": bool(v[8]), "filter_mfma": v[9]}
+                "train_operands_cached": bool(v[8]), "filter_mfma": v[9],
+                "queries_per_wave": v[10]}
 
 
 def comm_unique_id():

@@ -113,7 +113,7 @@ struct knn_ctx {
     bool stage_open = false;  // the last stage_begin recorded an event (profile = 3 skips some)
     std::vector<float> stage_ms;
     std::vector<const char*> stage_names;
-    int64_t stats[10] = {0, 0, 0, -1, 0, 0, 0, 0, 0, 0};  // candidates, fallback queries, segments, filter
+    int64_t stats[11] = {0, 0, 0, -1, 0, 0, 0, 0, 0, 0, 0};  // candidates, fallback queries, segments, filter
                                                       // operand type, rerun, fused, train / query H2D
                                                       // bytes, train-side filter operands from the cache
     int subs = 2;                           // candidate sub-slices per segment of the last GEMM pass
@@ -720,6 +720,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         c->stats[3] = felem;
         c->stats[5] = fused;
         c->stats[9] = fused ? (plan.m16 ? 16 : 32) : 0;
+        c->stats[10] = fused ? 32 * plan.qg : 0;
         c->subs = subs;
     } else {
         c->rerun_stats[0] = nseg;
@@ -926,7 +927,7 @@ knn_dataset offset_rows(const knn_dataset& x, int64_t r0, int64_t n) {
 
 void reset_stats(knn_ctx* c) {
     c->stages.clear();
-    for (int i = 0; i < 10; i++) c->stats[i] = 0;
+    for (int i = 0; i < 11; i++) c->stats[i] = 0;
     c->stats[3] = -1;
 }
 
@@ -1188,7 +1189,7 @@ int32_t knn_stage_times(const knn_ctx* c, const char** names, float* ms, int32_t
 
 int32_t knn_last_stats(const knn_ctx* c, int64_t* out, int32_t n) {
     if (!c || !out) return 0;
-    int32_t m = std::min(n, 10);
+    int32_t m = std::min(n, 11);
     for (int32_t i = 0; i < m; i++) out[i] = c->stats[i];
     return m;
 }

@@ -335,3 +335,46 @@ def test_fused16_shapes_vs_oracle(knn, oracle, dtype, d, k, monkeypatch):
         assert np.array_equal(got[2][qs], oidx) and np.array_equal(got[0][qs], opred)
         assert np.array_equal(got[1][qs], odist.view(np.uint32))
         assert _same(got, ref)
+
+
+def test_fused_query_shape_fill_rule(knn, oracle, monkeypatch):
+    """knn_fused_plan's round-6 rule: 64 queries per wave (QG = 2) once its 512-query blocks,
+    at most max_splits pieces per query tile (the candidate lists' capacity), fill 80 % of the
+    CUs -- below that, 32 per wave.  Both sizes give the oracle's top-k and predictions on a
+    sample (main.cpp:40-82) and, on every query, the same results as the forced other shape;
+    knn_last_stats()[10] reports the shape."""
+    import math
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    nt, d, k = 200_000 + 13, 128, 10
+
+    def max_pieces():  # knn_capi.cpp max_splits, cap = 64 * KNN_RESCORE_CAPW (32)
+        best, cap = 1, 64 * 32
+        for s in range(2, 9):
+            e = k * (1.0 + math.log(max(nt / s / k, 1.0))) + 64.0
+            if 1.5 * (0.5 * e + 32.0) > cap // s // 2:
+                break
+            best = s
+        return best
+
+    tiles_needed = -(-4 * cus // (5 * max_pieces()))  # query tiles of 512 for an 80 % fill
+    for nq in (max(512 * (tiles_needed - 8), 1_000) + 7, 512 * (tiles_needed + 4) + 7):
+        want = 64 if (nq + 511) // 512 * max_pieces() * 5 >= 4 * cus or nq >= 384 * cus else 32
+        train, labels, test = _rows(knn, nt, nq, d, 37, "f32")
+        trf, lab, tef = train.float().cpu().numpy(), labels.cpu().numpy(), test.float().cpu().numpy()
+        qs = np.linspace(0, nq - 1, 24).astype(np.int64)
+        bad, opred, odist, oidx = oracle.knn(trf, lab, tef[qs], k, 10)
+        assert bad == 0
+        monkeypatch.delenv("KNN_FUSED_QG", raising=False)
+        c = knn.Context(0, algo="gemm_bf16")
+        got = _call(c, train, labels, test, k)
+        c.close()
+        assert got[3]["fused_norm"] and got[3]["queries_per_wave"] == want, (nq, got[3])
+        assert np.array_equal(got[2][qs], oidx) and np.array_equal(got[0][qs], opred)
+        assert np.array_equal(got[1][qs], odist.view(np.uint32))
+        monkeypatch.setenv("KNN_FUSED_QG", "1" if want == 64 else "2")
+        c = knn.Context(0, algo="gemm_bf16")
+        other = _call(c, train, labels, test, k)
+        c.close()
+        assert other[3]["queries_per_wave"] == 96 - want
+        assert _same(got, other)
