@@ -158,7 +158,8 @@ knn_status knn_predict(knn_ctx* ctx, const knn_dataset* train, const knn_dataset
 /*
  * Device-buffer entry point (inputs already resident in HBM): all pointers in the
  * datasets and outputs are device pointers on ctx's device; work is enqueued on
- * `hip_stream` (a hipStream_t; NULL = the context's own stream).  Returns after
+ * `hip_stream` (a hipStream_t; NULL = the context's own stream, a blocking stream: ordered
+ * after work issued earlier on the legacy null stream).  Returns after
  * the stream has drained and the device-side status word was checked.
  */
 knn_status knn_predict_device(knn_ctx* ctx, const knn_dataset* train, const knn_dataset* test,

@@ -212,7 +212,10 @@ def _stream_arg(stream, tensor):
     outputs, with no extra synchronisation."""
     if stream is None and tensor is not None and getattr(tensor, "is_cuda", False):
         import torch
-        stream = torch.cuda.current_stream(tensor.device).cuda_stream
+        # (the raw handle: 0.08 us per call against 1.9 for a torch.cuda.Stream object, on a
+        # ~0.1 ms config-L call; scripts/diag_call_overhead.py)
+        raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        stream = raw(tensor.device.index) if raw is not None else torch.cuda.current_stream(tensor.device).cuda_stream
     return None if stream is None else ctypes.c_void_p(stream)
 
 
@@ -368,11 +371,15 @@ class Context:
                                          q_begin, q_end, _ptr(pred), _ptr(dist), _ptr(idx)))
         return (pred, dist, idx) if topk else pred
 
-    def _stream(self, stream, tensor):
-        """_stream_arg, after checking that the tensor lives on this context's device (a call
-        on another device's stream fails inside HIP with an unhelpful error)."""
+    def _on_device(self, tensor):
+        """The tensor lives on this context's device (a call on another device's stream fails
+        inside HIP with an unhelpful error)."""
         if tensor is not None and getattr(tensor, "is_cuda", False) and tensor.device.index != self.device:
             raise KnnError(KNN_EINVAL, f"tensor on cuda:{tensor.device.index}, context on device {self.device}")
+
+    def _stream(self, stream, tensor):
+        """_stream_arg, after _on_device."""
+        self._on_device(tensor)
         return _stream_arg(stream, tensor)
 
     def _note_train(self, train):
@@ -401,7 +408,7 @@ class Context:
         With cache_train the train-side filter operands are kept across calls on the same,
         unmodified train tensor (rewrites through torch are seen; after writing it by other
         means call set_generation)."""
-        self._stream(None, train)
+        self._on_device(train)
         self._note_train(train)
         tr = _device_dataset(train, labels, d)
         te = _device_dataset(test, None, d)
@@ -414,7 +421,7 @@ class Context:
     def shard_topk_device(self, train, labels, test, k, num_classes, idx_base, rec, stream=None, d=None):
         """Exact k nearest rows of one train shard for every query (knn_shard_topk_device).
         rec: int32 device tensor [nq][3][k] <- (dist bits, idx_base + row, label), ascending."""
-        self._stream(None, train)
+        self._on_device(train)
         self._note_train(train)
         tr = _device_dataset(train, labels, d)
         te = _device_dataset(test, None, d)
@@ -580,7 +587,7 @@ class Comm:
                               stream=None, d=None):
         """knn_predict_train_sharded: this rank's train shard (global rows [idx_base, ...)) and
         every query in, the owned queries' (shard_range) predictions out."""
-        self.ctx._stream(None, shard)
+        self.ctx._on_device(shard)
         self.ctx._note_train(shard)
         tr = _device_dataset(shard, labels, d)
         te = _device_dataset(test, None, d)

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -89,7 +90,9 @@ struct knn_ctx {
     bool no_lshare = false, no_cursor = false, rescore_all = false;
     // host-API staging (device copies of host inputs / outputs)
     DBuf h_train, h_labels, h_test, h_pred, h_dist, h_idx;
-    int32_t* ctrl_host = nullptr;  // pinned, mapped, fine-grained: [0] status, [1] fallback count
+    int32_t* ctrl_host = nullptr;  // pinned, mapped, fine-grained: [0] status, [1] fallback count,
+                                   // [4] the sequence number of the last k_finish
+    uint32_t finish_seq = 0;
     int32_t* ctrl_host_dev = nullptr;  // its device address (k_finish writes it)
     bool ctrl_clean = false;  // the status words are zero (the last call ended in k_finish)
     DBuf arrive;              // k_direct_rows' fused merge: per query group, segments finished
@@ -254,10 +257,26 @@ knn_status check_status(knn_ctx* c, const int32_t* ctrl) {
 }
 
 // the one host synchronisation of a call: k_finish writes the status words to the host's
-// mapped copy and zeroes them for the next call, then the stream drains
+// mapped copy and zeroes them for the next call, then the stream drains.  The host first spins
+// (up to 200 us) on the sequence word k_finish writes last: a short call returns ~6 us sooner
+// than through hipStreamSynchronize, whose completion signal costs ~12 us per wait even for a
+// finished stream (scripts/diag/sync_latency.hip, profiles/r06_studies/r06sync.log).  Longer
+// calls, and profile mode (its events are read through the runtime), end in the stream sync.
 knn_status finish_call(knn_ctx* c, hipStream_t st) {
-    HIP_OR_FAIL(c, knn_launch_finish(c->ctrl.as<int32_t>(), c->ctrl_host_dev, 4, st));
-    HIP_OR_FAIL(c, hipStreamSynchronize(st));
+    const uint32_t seq = ++c->finish_seq;
+    HIP_OR_FAIL(c, knn_launch_finish(c->ctrl.as<int32_t>(), c->ctrl_host_dev, 4, seq, st));
+    bool done = false;
+    if (!c->profile) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int spin = 0;; spin++) {
+            if ((uint32_t)__atomic_load_n(c->ctrl_host + 4, __ATOMIC_ACQUIRE) == seq) {
+                done = true;
+                break;
+            }
+            if ((spin & 63) == 63 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) break;
+        }
+    }
+    if (!done) HIP_OR_FAIL(c, hipStreamSynchronize(st));
     c->ctrl_clean = true;
     c->arrive_clean = true;  // every query group's merging wave reset its counter
     collect_stages(c);
@@ -773,9 +792,12 @@ knn_status knn_create(knn_ctx** out, const knn_opts* opts) {
         return KNN_ENODEV;
     }
     c->num_cus = prop.multiProcessorCount;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+    // the context's own stream (device calls given no stream) is a BLOCKING stream: ordered after
+    // the work the caller issued on the legacy null stream (torch's default stream), as the
+    // device entry points promise; the copy stream of the host pipeline stays non-blocking
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess ||
         hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void**)&c->ctrl_host, 4 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+        hipHostMalloc((void**)&c->ctrl_host, 8 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
             hipSuccess ||
         hipHostGetDevicePointer((void**)&c->ctrl_host_dev, c->ctrl_host, 0) != hipSuccess ||
         c->ctrl.ensure(4 * sizeof(int32_t)) != hipSuccess) {

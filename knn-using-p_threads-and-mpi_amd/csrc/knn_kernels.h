@@ -175,7 +175,7 @@ hipError_t knn_launch_round_rows(const float* x, int64_t n, int ld, int d, uint1
                                  const int32_t* gate = nullptr);
 hipError_t knn_launch_fill_u32(uint32_t* p, int64_t n, uint32_t v, const int32_t* gate, hipStream_t st);
 // host_mapped[0..n) = ctrl[0..n) (a mapped pinned host buffer), then ctrl[0..n) = 0
-hipError_t knn_launch_finish(int32_t* ctrl, int32_t* host_mapped, int n, hipStream_t st);
+hipError_t knn_launch_finish(int32_t* ctrl, int32_t* host_mapped, int n, uint32_t seq, hipStream_t st);
 // AUTO's re-run decision on the device: ctrl[3] = !unsafe && ctrl[1] > limit (and ctrl[1] = 0 then)
 hipError_t knn_launch_rerun_decide(int32_t* ctrl, int64_t limit, hipStream_t st);
 hipError_t knn_launch_rescore(const RescoreArgs& a, hipStream_t st);

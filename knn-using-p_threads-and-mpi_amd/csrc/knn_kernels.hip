@@ -2090,17 +2090,26 @@ __global__ void k_rerun_decide(int32_t* ctrl, int64_t limit) {
 
 // The end of a call: the status words go straight to the host's mapped (fine-grained) copy and
 // are reset for the next call -- one tiny kernel instead of a device-to-host copy (a DMA-engine
-// round trip) plus the next call's memset of the words.
-__global__ __launch_bounds__(64) void k_finish(int32_t* __restrict__ ctrl, int32_t* __restrict__ host, int n) {
+// round trip) plus the next call's memset of the words.  Then host[n] = seq, after a system-
+// scope release: the host waits for that word (finish_call) instead of the stream's completion
+// signal.  Every earlier kernel of the stream has completed, its end-of-kernel release included,
+// before this one starts (in-order stream: barrier bit set).
+__global__ __launch_bounds__(64) void k_finish(int32_t* __restrict__ ctrl, int32_t* __restrict__ host, int n,
+                                               uint32_t seq) {
     const int i = threadIdx.x;
     if (i < n) {
         host[i] = ctrl[i];
         ctrl[i] = 0;
     }
+    __syncthreads();
+    if (i == 0) {
+        __threadfence_system();
+        __hip_atomic_store(host + n, (int32_t)seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
-hipError_t knn_launch_finish(int32_t* ctrl, int32_t* host_mapped, int n, hipStream_t st) {
-    hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, st, ctrl, host_mapped, n);
+hipError_t knn_launch_finish(int32_t* ctrl, int32_t* host_mapped, int n, uint32_t seq, hipStream_t st) {
+    hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, st, ctrl, host_mapped, n, seq);
     KNN_LAUNCH_CHECK();
     return hipSuccess;
 }

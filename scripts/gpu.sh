@@ -59,7 +59,7 @@ if [ "$TESTS" = 1 ]; then
 fi
 
 for cfg in $BENCHES; do
-  extra=""; [ "$cfg" = L ] && extra="--steps 50 --warmup 5"
+  extra=""
   timeout -k 10 600 python -u bench.py --config $cfg $extra > gpurun_out/${TAG}_bench_$cfg.log 2>&1 \
       || { echo "bench $cfg failed"; tail -5 gpurun_out/${TAG}_bench_$cfg.log; exit 1; }
   echo "$cfg: $(tail -1 gpurun_out/${TAG}_bench_$cfg.log | cut -c1-300)"

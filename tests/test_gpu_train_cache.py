@@ -378,3 +378,29 @@ def test_fused_query_shape_fill_rule(knn, oracle, monkeypatch):
         c.close()
         assert other[3]["queries_per_wave"] == 96 - want
         assert _same(got, other)
+
+
+def test_device_calls_use_torch_current_stream(knn):
+    """A device call with no stream argument is enqueued on torch's current stream of the
+    tensor's device (_stream_arg: the raw handle), also under a `torch.cuda.stream` context, so
+    it is ordered after the torch work that made its inputs; results equal the default stream's."""
+    import torch
+    x = torch.zeros((8, 16), device=DEV)
+    # (torch's default stream is the legacy null stream, handle 0: the call then runs on the
+    # context's own stream, which is a blocking stream -- ordered after null-stream work)
+    assert (knn._stream_arg(None, x).value or 0) == torch.cuda.current_stream().cuda_stream
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        assert knn._stream_arg(None, x).value == s.cuda_stream
+    train, labels, test = _rows(knn, 5_000, 300, 16, 41)
+    c = knn.Context(0)
+    try:
+        ref = _call(c, train, labels, test, 5)
+        with torch.cuda.stream(s):
+            t2 = test * 1.0  # made on s: the call must be ordered after it
+            got = _call(c, train, labels, t2, 5)
+        assert _same(ref, got)
+        t3 = test * 1.0  # made on the null stream, no synchronisation before the call
+        assert _same(ref, _call(c, train, labels, t3, 5))
+    finally:
+        c.close()
