@@ -274,6 +274,7 @@ knn_status finish_call(knn_ctx* c, hipStream_t st) {
                 break;
             }
             if ((spin & 63) == 63 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) break;
+            __builtin_ia32_pause();  // (x86-64 host: yield the core's pipeline to its sibling thread)
         }
     }
     if (!done) HIP_OR_FAIL(c, hipStreamSynchronize(st));
