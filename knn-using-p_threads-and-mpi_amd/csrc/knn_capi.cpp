@@ -1128,6 +1128,31 @@ knn_status knn_predict(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te,
         if (out_dist) HIP_OR_ABORT(c->dist_slot[i].ensure(sizeof(float) * B * k));
         if (out_idx) HIP_OR_ABORT(c->idx_slot[i].ensure(sizeof(int32_t) * B * k));
     }
+    if (nb == 1) {
+        // one batch (a call of config L's size): one stream and no events -- the upload, the pass,
+        // k_finish's status hand-off (finish_call: the spin on its sequence word), then the
+        // downloads.  The pipelined form below pays three cross-stream event waits and a status
+        // copy per batch, which only pay off when batches overlap.
+        const unsigned char* src = (const unsigned char*)te->feat + es * (size_t)q_begin * (size_t)te->ld;
+        HIP_OR_ABORT(hipMemcpy2DAsync(c->q_slot[0].p, es * ldd, src, es * te->ld, es * d, nq, hipMemcpyHostToDevice, st));
+        c->stats[7] += (int64_t)(es * d * nq);
+        const knn_dataset dq{c->q_slot[0].p, nullptr, nq, d, ldd, te->dtype};
+        const QueryOut o{c->pred_slot[0].as<int32_t>(), out_dist ? c->dist_slot[0].as<float>() : nullptr,
+                         out_idx ? c->idx_slot[0].as<int32_t>() : nullptr, nullptr, k, 0};
+        if ((s = predict_enqueue(c, &dtr, &dq, k, C, o, st, algo, nullptr)) != KNN_OK) return abort_call(s);
+        if ((s = finish_call(c, st)) != KNN_OK) {
+            if (s != KNN_EINVAL && s != KNN_ERANGE) return abort_call(s);
+            return s;  // (a status error: every kernel of the call has completed)
+        }
+        // (synchronous copies on the null stream: ordered after the context's blocking stream)
+        HIP_OR_ABORT(hipMemcpy(out_pred, c->pred_slot[0].p, sizeof(int32_t) * nq, hipMemcpyDeviceToHost));
+        if (out_dist)
+            HIP_OR_ABORT(hipMemcpy(out_dist, c->dist_slot[0].p, sizeof(float) * nq * k, hipMemcpyDeviceToHost));
+        if (out_idx)
+            HIP_OR_ABORT(hipMemcpy(out_idx, c->idx_slot[0].p, sizeof(int32_t) * nq * k, hipMemcpyDeviceToHost));
+        pass_stats(c, c->ctrl_host, gemm);
+        return KNN_OK;
+    }
     while ((int64_t)c->ctrl_slots.size() < nb) {
         int32_t* p = nullptr;
         HIP_OR_ABORT(hipHostMalloc((void**)&p, 4 * sizeof(int32_t), hipHostMallocDefault));
