@@ -441,11 +441,11 @@ void certificate_fused(int d, bool /*rounded*/, float* coef, float* eta) {
     *eta = (float)(8 * d + 16) * 0x1p-125f;
 }
 
-// the most train segments (or schedule pieces) per query tile whose expected kept rows fit
-// their slice of the candidate list (choose_splits' rule)
-int max_splits(int64_t nt, int k, int cap) {
+// the most train segments (or schedule pieces) per query tile, at most smax, whose expected
+// kept rows fit their slice of the candidate list (choose_splits' rule)
+int max_splits(int64_t nt, int k, int cap, int smax = 8) {
     int best = 1;
-    for (int s = 2; s <= 8; s++) {
+    for (int s = 2; s <= smax; s++) {
         const double rows = (double)nt / s;
         const double expect = k * (1.0 + std::log(std::max(rows / k, 1.0))) + 64.0;
         if (1.5 * (0.5 * expect + 32.0) > (double)(cap / s / 2)) break;
@@ -455,7 +455,7 @@ int max_splits(int64_t nt, int k, int cap) {
 }
 
 int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int rb, int k, int cap,
-                  bool fused = false, int d = 0, const FilterPlan* fplan = nullptr) {
+                  bool fused = false, int d = 0, const FilterPlan* fplan = nullptr, int smax = 8) {
     if (c->train_splits > 0) return std::min(8, c->train_splits);
     // More segments shrink the partial last wave of blocks (measured on config A:
     // S=3 224 ms, S=5 217 ms, S=8 216 ms), but each segment must fit its rows in its
@@ -469,7 +469,7 @@ int choose_splits(const knn_ctx* c, int64_t n_qtiles, int64_t nt, int dtype, int
     const int64_t slots = (int64_t)occ * c->num_cus;
     int best = 1;
     double best_eff = 0.0;
-    for (int s = 1; s <= 8; s++) {
+    for (int s = 1; s <= smax; s++) {
         const double rows = (double)nt / s;
         if (s > 1 && rows < 64 * 64) break;
         const double expect = k * (1.0 + std::log(std::max(rows / k, 1.0))) + 64.0;
@@ -495,19 +495,28 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     const int felem = filter_elem(algo, dtype);  // the filter's operand type
     const int rb = filter_row_bytes(felem, d);
     const int kelem = felem == ELEM_ROUND ? ELEM_BF16 : felem;  // ELEM_ROUND runs the bf16 kernel
-    const int cap = 64 * KNN_RESCORE_CAPW;
+    // Small query sets (round 6): a candidate list 2-4x as long per query, so the filter may cut
+    // each query tile into up to 16 pieces (32 sub-slices, k_rescore's limit) and fill the CUs
+    // -- a 3,125-query call on A's rows ran 13 query tiles x 5 pieces on 256 CUs.  The
+    // workspace stays within 512 MiB.  (The 16x16x32 study filter's quarter lists: 8 pieces.)
+    const size_t per_q = 12 * 64 * (size_t)KNN_RESCORE_CAPW;
+    const int capmul = c->fforce.m16 ? 1
+                     : (size_t)nq * per_q * 4 <= ((size_t)512 << 20) ? 4
+                     : (size_t)nq * per_q * 2 <= ((size_t)512 << 20) ? 2 : 1;
+    const int cap = 64 * KNN_RESCORE_CAPW * capmul;
+    const int smax = capmul > 1 ? 16 : 8;
     HIP_OR_FAIL(c, c->tnorm.ensure(sizeof(float) * (nt + 64)));
     HIP_OR_FAIL(c, c->tnp.ensure(sizeof(float) * (nt + 64)));
     HIP_OR_FAIL(c, c->qnorm.ensure(sizeof(float) * nq));
     HIP_OR_FAIL(c, c->gthr.ensure(sizeof(uint32_t) * nq));
-    HIP_OR_FAIL(c, c->cnt.ensure(sizeof(int32_t) * nq * 32));  // [subs * nseg][nq], subs <= 4, nseg <= 8
+    HIP_OR_FAIL(c, c->cnt.ensure(sizeof(int32_t) * nq * 32));  // [subs * nseg][nq], subs * nseg <= 32
     HIP_OR_FAIL(c, c->cand.ensure(sizeof(CandRec) * nq * cap));
     HIP_OR_FAIL(c, c->fb_list.ensure(sizeof(int32_t) * nq));
 
     // bf16 MFMA operands (rounded fp32 rows or bf16 data) run the fused-norm filter
     // the fused filter's plan, computed once: it sizes the tile blocks (bn_f), the occupancy,
     // the schedule and the launch of this pass
-    const FilterPlan fplan = knn_fused_supported(d) ? knn_fused_plan(d, k, nq, c->num_cus, c->fforce, max_splits(nt, k, cap)) : FilterPlan{};
+    const FilterPlan fplan = knn_fused_supported(d) ? knn_fused_plan(d, k, nq, c->num_cus, c->fforce, max_splits(nt, k, cap, smax)) : FilterPlan{};
     const bool fused = (felem == ELEM_ROUND || felem == ELEM_BF16) && knn_fused_supported(d) && fplan.nw > 0;
     float coef, eta;
     if (fused) {
@@ -663,10 +672,10 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
         if (knn_fused_occupancy(d, plan, &occ) != hipSuccess || occ < 1) occ = 1;
         int nb = 1;
         knn_fused_schedule(g, occ * c->num_cus, &nb);
-        if (nb <= max_splits(nt, k, cap)) nseg = nb;
+        if (nb <= max_splits(nt, k, cap, smax)) nseg = nb;
     }
     if (nseg == 0) {
-        nseg = choose_splits(c, n_qtiles, nt, kelem, rb, k, cap, fused, d, &plan);
+        nseg = choose_splits(c, n_qtiles, nt, kelem, rb, k, cap, fused, d, &plan, smax);
         g.g2 = -1;  // segment schedule
     }
     int64_t seg_len = (nt + nseg - 1) / nseg;

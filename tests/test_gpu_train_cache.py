@@ -404,3 +404,29 @@ def test_device_calls_use_torch_current_stream(knn):
         assert _same(ref, _call(c, train, labels, t3, 5))
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("dtype,d,k", [("f32", 128, 10), ("f32", 64, 32), ("bf16", 256, 100)])
+def test_small_query_sets_many_pieces(knn, oracle, dtype, d, k):
+    """Round 6: a small query set gets a 2-4x candidate list per query, so the filter cuts each
+    query tile into up to 16 pieces (32 candidate sub-slices in k_rescore) to fill the CUs.  The
+    results equal the oracle's on a sample (main.cpp:40-82) and the exact scan's on every
+    query, ties and all."""
+    nt, nq = 300_000 + 29, 1_200 + 5
+    train, labels, test = _rows(knn, nt, nq, d, 43, dtype)
+    trf, lab, tef = train.float().cpu().numpy(), labels.cpu().numpy(), test.float().cpu().numpy()
+    qs = np.linspace(0, nq - 1, 16).astype(np.int64)
+    bad, opred, odist, oidx = oracle.knn(trf, lab, tef[qs], k, 10)
+    assert bad == 0
+    c = knn.Context(0, algo="gemm_bf16")
+    got = _call(c, train, labels, test, k)
+    c.close()
+    assert got[3]["fused_norm"] and got[3]["fallback_queries"] == 0, got[3]
+    # more pieces than a list of the base length allows (k = 100: 6 against 1)
+    assert got[3]["train_segments"] > (8 if k <= 32 else 1), got[3]
+    assert np.array_equal(got[2][qs], oidx) and np.array_equal(got[0][qs], opred)
+    assert np.array_equal(got[1][qs], odist.view(np.uint32))
+    c = knn.Context(0, algo="direct_scan")
+    ref = _call(c, train, labels, test, k)
+    c.close()
+    assert _same(got, ref)
