@@ -495,14 +495,19 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     const int felem = filter_elem(algo, dtype);  // the filter's operand type
     const int rb = filter_row_bytes(felem, d);
     const int kelem = felem == ELEM_ROUND ? ELEM_BF16 : felem;  // ELEM_ROUND runs the bf16 kernel
-    // Small query sets (round 6): a candidate list 2-4x as long per query, so the filter may cut
-    // each query tile into up to 16 pieces (32 sub-slices, k_rescore's limit) and fill the CUs
-    // -- a 3,125-query call on A's rows ran 13 query tiles x 5 pieces on 256 CUs.  The
-    // workspace stays within 512 MiB.  (The 16x16x32 study filter's quarter lists: 8 pieces.)
-    const size_t per_q = 12 * 64 * (size_t)KNN_RESCORE_CAPW;
-    const int capmul = c->fforce.m16 ? 1
-                     : (size_t)nq * per_q * 4 <= ((size_t)512 << 20) ? 4
-                     : (size_t)nq * per_q * 2 <= ((size_t)512 << 20) ? 2 : 1;
+    // Small query sets (round 6): when the base list's pieces would leave CUs idle (256-query
+    // tiles x max_splits pieces under 80 % of the CUs -- a 3,125-query call on A's rows ran 13
+    // tiles x 5 pieces on 256 CUs), a candidate list 2-4x as long per query, so the filter may
+    // cut each query tile into up to 16 pieces (32 sub-slices, k_rescore's limit).  The
+    // workspace stays within 1.5 GiB.  The queries-per-wave choice (knn_fused_plan) still
+    // counts the base list's pieces: 64-query waves cut into more than ~5 pieces lost to the
+    // 32-query shape (A's rows, 6,250 queries: 2.06 against 1.84 ms, r06bh).  (The 16x16x32
+    // study filter's quarter lists: 8 pieces.)
+    const size_t per_q = 12 * 64 * (size_t)KNN_RESCORE_CAPW, ws_lim = (size_t)1536 << 20;
+    const bool idle = (nq + 255) / 256 * (int64_t)max_splits(nt, k, 64 * KNN_RESCORE_CAPW) * 5 < (int64_t)4 * c->num_cus;
+    const int capmul = (c->fforce.m16 || !idle) ? 1
+                     : (size_t)nq * per_q * 4 <= ws_lim ? 4
+                     : (size_t)nq * per_q * 2 <= ws_lim ? 2 : 1;
     const int cap = 64 * KNN_RESCORE_CAPW * capmul;
     const int smax = capmul > 1 ? 16 : 8;
     HIP_OR_FAIL(c, c->tnorm.ensure(sizeof(float) * (nt + 64)));
@@ -516,7 +521,7 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     // bf16 MFMA operands (rounded fp32 rows or bf16 data) run the fused-norm filter
     // the fused filter's plan, computed once: it sizes the tile blocks (bn_f), the occupancy,
     // the schedule and the launch of this pass
-    const FilterPlan fplan = knn_fused_supported(d) ? knn_fused_plan(d, k, nq, c->num_cus, c->fforce, max_splits(nt, k, cap, smax)) : FilterPlan{};
+    const FilterPlan fplan = knn_fused_supported(d) ? knn_fused_plan(d, k, nq, c->num_cus, c->fforce, max_splits(nt, k, 64 * KNN_RESCORE_CAPW)) : FilterPlan{};
     const bool fused = (felem == ELEM_ROUND || felem == ELEM_BF16) && knn_fused_supported(d) && fplan.nw > 0;
     float coef, eta;
     if (fused) {
@@ -667,7 +672,11 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     // fused filter: the balanced schedule (knn_fused_schedule) when its pieces per query tile
     // fit the candidate list like segments do; else (or with explicit train_splits) segments
     int nseg = 0;
-    if (fused && c->train_splits <= 0) {
+    // (the balanced schedule's ranges span two query tiles, a piece of each, so a block may pay
+    // two threshold warm-ups; with the longer lists of small query sets (capmul > 1), whose
+    // pieces are many and short, the even segments measured faster: A's rows, 6,250 queries,
+    // 2.02 against 1.84 ms, r06bi)
+    if (fused && c->train_splits <= 0 && capmul == 1) {
         int occ = 1;
         if (knn_fused_occupancy(d, plan, &occ) != hipSuccess || occ < 1) occ = 1;
         int nb = 1;
