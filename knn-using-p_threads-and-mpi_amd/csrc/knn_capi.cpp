@@ -226,15 +226,15 @@ int choose_algo(const knn_ctx* c, int64_t nt, int64_t nq, int d, int k, int dtyp
     // AUTO: the direct form wins at low d (3 VALU ops per dim, no rescore) and on small jobs;
     // above that the rounded bf16 filter (one MFMA per 16 features), re-run as split when
     // its wider certificate overflows the candidate lists (predict_core).  For the fused
-    // filter's widths (d = 64, 128, 256) "small" is now a few million pairs on at least 16k
-    // rows (round 6, with the small-set pieces): same box, ms per call direct -> filter, d = 128:
-    // 100k x 100 rows 1.07 -> 0.27, 30k x 300 0.41 -> 0.26, 100k x 1000 1.38 -> 0.35, 1M x 500
-    // 8.72 -> 1.07; d = 64, k = 32: 50k x 200 0.61 -> 0.37, 100k x 2000 2.51 -> 0.49; at 10k
-    // rows the two are equal (0.21-0.26), and the direct form wins there at d = 64, k = 32
-    // (0.25 vs 0.31; profiles/r06_studies/r06au).  Other widths keep the 10^9-pair rule.
+    // filter's widths (d = 64, 128, 256) "small" now means under 16k rows (round 6, with the
+    // small-set pieces): same box, ms per call direct -> filter, d = 128 (rows x queries): 1M x 1
+    // 11.7 -> 0.78, 1M x 64 13.0 -> 0.87, 100k x 100 1.07 -> 0.27, 30k x 300 0.41 -> 0.26, 100k x
+    // 1000 1.38 -> 0.35, 1M x 500 8.72 -> 1.07; d = 64, k = 32: 50k x 200 0.61 -> 0.37, 100k x
+    // 2000 2.51 -> 0.49; 20k x 150 0.29 either way; at 10k rows the two are equal (0.21-0.26)
+    // and the direct form wins at d = 64, k = 32 (0.25 vs 0.31; profiles/r06_studies/r06au).
+    // Other widths keep the 10^9-pair rule.
     const double pairs = (double)nt * (double)nq;
-    if (d >= 32 && nt >= 8192 &&
-        (pairs >= 1e9 || (knn_fused_supported(d) && nt >= 16384 && pairs >= 4e6))) {
+    if (d >= 32 && nt >= 8192 && (pairs >= 1e9 || (knn_fused_supported(d) && nt >= 16384))) {
         if (gemm_ok(KNN_ALGO_GEMM_BF16)) return KNN_ALGO_GEMM_BF16;
         if (gemm_ok(KNN_ALGO_GEMM_SPLIT)) return KNN_ALGO_GEMM_SPLIT;
         if (gemm_ok(KNN_ALGO_GEMM)) return KNN_ALGO_GEMM;
