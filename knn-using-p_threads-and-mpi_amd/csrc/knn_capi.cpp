@@ -506,23 +506,28 @@ knn_status run_gemm(knn_ctx* c, const knn_dataset* tr, const knn_dataset* te, in
     // Small query sets (round 6): when the base list's pieces would leave CUs idle (256-query
     // tiles x max_splits pieces under 80 % of the CUs -- a 3,125-query call on A's rows ran 13
     // tiles x 5 pieces on 256 CUs), a candidate list 2-4x as long per query, so the filter may
-    // cut each query tile into up to 16 pieces (32 sub-slices, k_rescore's limit).  The
+    // cut each query tile into up to 16 pieces (32 candidate sub-slices; 32 pieces for the tiny
+    // sets below, 64 sub-slices, k_rescore's limit).  The
     // workspace stays within 1.5 GiB.  The queries-per-wave choice (knn_fused_plan) still
     // counts the base list's pieces: 64-query waves cut into more than ~5 pieces lost to the
     // 32-query shape (A's rows, 6,250 queries: 2.06 against 1.84 ms, r06bh).  (The 16x16x32
     // study filter's quarter lists: 8 pieces.)
     const size_t per_q = 12 * 64 * (size_t)KNN_RESCORE_CAPW, ws_lim = (size_t)1536 << 20;
     const bool idle = (nq + 255) / 256 * (int64_t)max_splits(nt, k, 64 * KNN_RESCORE_CAPW) * 5 < (int64_t)4 * c->num_cus;
+    // (a handful of query tiles, idle even at 16 pieces each -- 1,000 queries: 4 tiles -- gets
+    // an 8x list and up to 32 pieces, 64 sub-slices)
+    const bool tiny = idle && (nq + 255) / 256 * 16 * 5 < (int64_t)4 * c->num_cus;
     const int capmul = (c->fforce.m16 || !idle) ? 1
+                     : tiny && (size_t)nq * per_q * 8 <= ws_lim ? 8
                      : (size_t)nq * per_q * 4 <= ws_lim ? 4
                      : (size_t)nq * per_q * 2 <= ws_lim ? 2 : 1;
     const int cap = 64 * KNN_RESCORE_CAPW * capmul;
-    const int smax = capmul > 1 ? 16 : 8;
+    const int smax = capmul == 8 ? 32 : capmul > 1 ? 16 : 8;
     HIP_OR_FAIL(c, c->tnorm.ensure(sizeof(float) * (nt + 64)));
     HIP_OR_FAIL(c, c->tnp.ensure(sizeof(float) * (nt + 64)));
     HIP_OR_FAIL(c, c->qnorm.ensure(sizeof(float) * nq));
     HIP_OR_FAIL(c, c->gthr.ensure(sizeof(uint32_t) * nq));
-    HIP_OR_FAIL(c, c->cnt.ensure(sizeof(int32_t) * nq * 32));  // [subs * nseg][nq], subs * nseg <= 32
+    HIP_OR_FAIL(c, c->cnt.ensure(sizeof(int32_t) * nq * 64));  // [subs * nseg][nq], subs * nseg <= 64
     HIP_OR_FAIL(c, c->cand.ensure(sizeof(CandRec) * nq * cap));
     HIP_OR_FAIL(c, c->fb_list.ensure(sizeof(int32_t) * nq));
 

@@ -1432,7 +1432,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_gemm_filter(GemmFilterArgs a)
 // the query's candidates; candidates with L <= threshold are rescored with the exact
 // direct form and selected by key.  Queries whose list overflowed (or holds < k entries)
 // go to the exact fallback list.
-//  * The candidates sit in a.nseg (<= 32) sub-slices of cap_seg entries; compact entry e
+//  * The candidates sit in a.nseg (<= 64) sub-slices of cap_seg entries; compact entry e
 //    maps to (slice, offset) through the slices' prefix sums.  Their ordered U bits are
 //    staged in LDS (su, <= 64 CAPW words), so the bisection reads only the entries that
 //    exist, in ceil(total / 64) ballots per round, and between the wave's smallest and
@@ -1465,7 +1465,7 @@ __device__ __forceinline__ void rescore_query(const RescoreArgs& a, const int64_
     float* qs = reinterpret_cast<float*>(my);
     int* counts = a.c_lds_bytes ? reinterpret_cast<int*>(my + a.q_lds_bytes) : nullptr;  // NULL: vote_ballot
     uint32_t* su = reinterpret_cast<uint32_t*>(my + a.q_lds_bytes + a.c_lds_bytes);
-    // sub-slice fills: lane sg < nseg holds slice sg's; inclusive prefix over lanes 0..31.
+    // sub-slice fills: lane sg < nseg (<= 64) holds slice sg's; inclusive prefix over the wave.
     // Read before the gate and status words (allocated either way), so the three loads
     // share one round trip.
     const int cs = lane < a.nseg ? a.cnt[(int64_t)lane * a.nq + q] : 0;
@@ -1483,11 +1483,11 @@ __device__ __forceinline__ void rescore_query(const RescoreArgs& a, const int64_
     const bool overflow = __ballot(cs > a.cap_seg) != 0ull;
     int incl = cs;
 #pragma unroll
-    for (int j = 1; j < 32; j <<= 1) {
+    for (int j = 1; j < 64; j <<= 1) {
         const int o = __shfl_up(incl, j);
-        if ((lane & 31) >= j) incl += o;
+        if (lane >= j) incl += o;
     }
-    const int total = __shfl(incl, 31);
+    const int total = __shfl(incl, 63);
     rstamp(1);
     if (overflow || total < k) {
         if (lane == 0) a.fb_list[atomicAdd(a.fb_count, 1)] = (int32_t)q;
@@ -1500,7 +1500,7 @@ __device__ __forceinline__ void rescore_query(const RescoreArgs& a, const int64_
     // candidate position of compact entry e: slice = last sg with excl[sg] <= e
     auto position = [&](int e) __attribute__((always_inline)) -> int64_t {
         int sg = 0, base = 0;
-        for (int s2 = 1; s2 < a.nseg; s2++) {  // uniform loop, <= 31 steps
+        for (int s2 = 1; s2 < a.nseg; s2++) {  // uniform loop, <= 63 steps
             const int ex = __builtin_amdgcn_readlane(excl, s2);
             if (e >= ex) { sg = s2; base = ex; }
         }
