@@ -45,6 +45,9 @@ static constexpr int FUSED_RQ = 4;            // queued passing values per lane 
 #ifndef KNN_FUSED_TF_GLOBAL
 #define KNN_FUSED_TF_GLOBAL 1                 // fast-test tile term from the maxima over all tiles (a.tsmax)
 #endif
+#ifndef KNN_FUSED_IDLE_SKIP
+#define KNN_FUSED_IDLE_SKIP 1                 // a wave with no valid query issues its tile DMAs and barriers only
+#endif
 #ifndef KNN_FUSED_DMA_FRONT
 #define KNN_FUSED_DMA_FRONT 0                 // (study) a group's tile DMAs all issued right after its barrier
 #endif
@@ -345,6 +348,13 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
         published[g] = thr[g];
         ccnt[g] = 0;
     }
+    // a wave whose queries all lie past nq (the last query tile; a few-query call's seven other
+    // waves) keeps the block's tile DMAs and barriers but runs no MFMAs or tests, so its SIMD
+    // partner has the matrix pipe to itself
+    bool any_q = false;
+#pragma unroll
+    for (int g = 0; g < QG; g++) any_q = any_q || qvalid[g];
+    const bool wave_live = !KNN_FUSED_IDLE_SKIP || KNN_FUSED_DMA_FRONT || __ballot(any_q) != 0ull;
     float root = INF;  // (heap shapes, QG = 1) this query's heap root, mirrored in both lanes
     float qe2[QG], eq2[QG];  // 2 |q| and 2 |q - rq|, rounded up
 #pragma unroll
@@ -1245,7 +1255,17 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
     };
     typedef std::integral_constant<int, 0> P0;
     typedef std::integral_constant<int, 1 % GRP> P1;
-    if constexpr (GRP == 8) {  // octets (the 64-query shape's default)
+    if (!wave_live) {
+        // (no valid query) the same barriers, and this wave's pieces of every tile's DMA
+        for (int it = 0; it < ntiles; it++) {
+            if (it % GRP == 0) wait_dma_barrier();
+            if (!KNN_STUDY_NO_DMA && it + AHEAD < ntiles) {
+                const DmaTile dd = dma_desc((it + AHEAD) % NBUF, it + AHEAD);
+#pragma unroll
+                for (int i = 0; i < DMA_PER_WAVE; i++) dma_piece(i, dd);
+            }
+        }
+    } else if constexpr (GRP == 8) {  // octets (the 64-query shape's default)
         for (int it = 0; it < ntiles; it += 8) {
             iter(P0{}, accA, accB, it);
             iter(P1{}, accB, accA, it + 1);
@@ -1269,7 +1289,7 @@ __device__ __forceinline__ void fused_piece(const GemmFilterArgs& a, const int q
             iter(P1{}, accB, accA, it + 1);
         }
     }
-    if (ntiles > 0) {
+    if (ntiles > 0 && wave_live) {
         // drain: the last tile's accumulators (ntiles is even: accB)
         const int last = ntiles - 1;
         if constexpr (TFG) tm_prev = tile_q(last % NBUF);  // (no DMA since: the buffer holds it)
