@@ -430,3 +430,27 @@ def test_small_query_sets_many_pieces(knn, oracle, dtype, d, k):
     ref = _call(c, train, labels, test, k)
     c.close()
     assert _same(got, ref)
+
+
+@pytest.mark.parametrize("nq", [1, 7, 33])
+def test_few_queries_idle_waves(knn, oracle, nq):
+    """A few-query call: one query tile whose other waves hold no valid query (they run only
+    the block's barriers and their tile-DMA pieces) cut into up to 32 pieces; every query
+    equals the oracle (main.cpp:40-82), for both query shapes."""
+    import os
+    nt, d, k = 100_000 + 17, 128, 10
+    train, labels, test = _rows(knn, nt, nq, d, 47, "f32")
+    trf, lab, tef = train.float().cpu().numpy(), labels.cpu().numpy(), test.float().cpu().numpy()
+    bad, opred, odist, oidx = oracle.knn(trf, lab, tef, k, 10)
+    assert bad == 0
+    for qg in ("1", "2"):
+        os.environ["KNN_FUSED_QG"] = qg
+        try:
+            c = knn.Context(0, algo="gemm_bf16")
+        finally:
+            del os.environ["KNN_FUSED_QG"]
+        got = _call(c, train, labels, test, k)
+        c.close()
+        assert got[3]["fused_norm"] and got[3]["queries_per_wave"] == 32 * int(qg), got[3]
+        assert np.array_equal(got[2], oidx) and np.array_equal(got[0], opred)
+        assert np.array_equal(got[1], odist.view(np.uint32))
